@@ -1,0 +1,85 @@
+"""ctypes binding of the C-ABI library (include/otamd.h).
+
+The product path has no CPU fallback: if libotamd.so is missing or does not load,
+every op raises.  Structs below mirror the C layouts; `check_layouts()` compares
+their sizes with the library's own sizeof() exports.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libotamd.so"
+
+OTAMD_OK, OTAMD_EINVAL, OTAMD_ELAUNCH, OTAMD_EUNSUPPORTED = 0, 1, 2, 3
+_ERR = {1: "invalid arguments (shape/alignment contract)", 2: "kernel launch failed", 3: "unsupported configuration"}
+
+
+class ConvGeom(C.Structure):
+    _fields_ = [("N", C.c_int), ("SH", C.c_int), ("SW", C.c_int), ("SC", C.c_int), ("RH", C.c_int),
+                ("RW", C.c_int), ("KH", C.c_int), ("KW", C.c_int), ("stride", C.c_int), ("pad", C.c_int),
+                ("upsample", C.c_int), ("pad_", C.c_int), ("ld", C.c_longlong)]
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [("A", C.c_void_p), ("lda", C.c_longlong), ("amode", C.c_int),
+                ("B", C.c_void_p), ("ldb", C.c_longlong), ("bmode", C.c_int),
+                ("C", C.c_void_p), ("ldc", C.c_longlong), ("c_f32", C.c_int), ("accumulate", C.c_int),
+                ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("alpha", C.c_float),
+                ("bias", C.c_void_p), ("rowvec", C.c_void_p), ("ldv", C.c_longlong), ("rows_per_vec", C.c_int),
+                ("residual", C.c_void_p), ("ldr", C.c_longlong), ("slab", C.c_void_p), ("k_per_split", C.c_int),
+                ("ga", ConvGeom), ("gb", ConvGeom)]
+
+
+class AdamwGroup(C.Structure):
+    _fields_ = [("begin", C.c_longlong), ("end", C.c_longlong), ("wd_factor", C.c_float),
+                ("one_minus_beta1", C.c_float), ("beta2", C.c_float), ("one_minus_beta2", C.c_float),
+                ("bc2_sqrt", C.c_float), ("eps", C.c_float), ("neg_step_size", C.c_float), ("pad", C.c_float)]
+
+
+class NormChunk(C.Structure):
+    _fields_ = [("begin", C.c_longlong), ("end", C.c_longlong), ("tensor", C.c_int), ("pad", C.c_int)]
+
+
+VP, I, LL, F, D = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
+
+# symbol -> argtypes (restype int).  Mirrors include/otamd.h one-for-one.
+SIGNATURES: dict[str, list] = {
+    "otamd_gemm_args_size": [],
+    "otamd_conv_geom_size": [],
+    "otamd_gemm": [C.POINTER(GemmArgs), I, VP, LL, VP],
+    "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
+    "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],
+    "otamd_grad_clip_coef": [VP, I, VP, I, VP, I, F, VP, VP],
+    "otamd_scale_bf16_by_device_scalar": [VP, LL, VP, VP],
+}
+
+_lib = None
+
+
+def lib():
+    """Load libotamd.so once.  Raises if it is absent: there is no fallback path."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"onetrainer_amd HIP library not built: {LIB_PATH} missing "
+                               "(run `python -m onetrainer_amd.build`); there is no CPU fallback")
+        L = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != OTAMD_OK:
+        raise RuntimeError(f"{what}: {_ERR.get(rc, 'error')} (status {rc})")
+
+
+def check_layouts():
+    L = lib()
+    assert L.otamd_gemm_args_size() == C.sizeof(GemmArgs), (L.otamd_gemm_args_size(), C.sizeof(GemmArgs))
+    assert L.otamd_conv_geom_size() == C.sizeof(ConvGeom)

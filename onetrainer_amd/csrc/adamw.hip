@@ -1,0 +1,275 @@
+// Fused AdamW + bf16 stochastic rounding and global grad-norm clipping over a
+// flat parameter store.  Replaces, per parameter tensor, the reference's
+//   modules/util/optimizer/adamw_extensions.py:17-150  (step_adamw_parameter)
+//   modules/util/bf16_stochastic_rounding.py:5-61     (copy/addcdiv_stochastic_)
+//   torch.nn.utils.clip_grad_norm_ called at modules/trainer/GenericTrainer.py:712-713
+// with ONE launch over the whole flat buffer (the reference runs ~8 torch ops per
+// tensor per step in a Python loop).
+//
+// Numerics: every torch op of the reference's bf16 path rounds its result to bf16;
+// this kernel applies the same roundings in the same order, with the same fused
+// multiply-adds torch's CPU kernels use (lerp and addcmul are fma; pinned in
+// tests/test_oracle_golden.py).  Compile with -ffp-contract=off so no other
+// contraction is introduced.
+//
+// HBM traffic per bf16 element: read p,g,m,v (8 B) + write p,m,v (6 B) = 14 B.
+#include "common.h"
+
+#define ADAMW_MAX_GROUPS 8
+
+struct AdamwGroup {
+  long long begin, end;     // element range [begin, end) of this group in the flat store
+  float wd_factor;          // 1 - lr * weight_decay           (p.mul_)
+  float one_minus_beta1;    // lerp weight                      (exp_avg.lerp_)
+  float beta2;              // exp_avg_sq.mul_(beta2)
+  float one_minus_beta2;    // addcmul value
+  float bc2_sqrt;           // sqrt(1 - beta2^step)
+  float eps;
+  float neg_step_size;      // -lr / (1 - beta1^step)
+  float pad;
+};
+struct AdamwGroups {
+  AdamwGroup g[ADAMW_MAX_GROUPS];
+  int n;
+};
+
+// counter-based 64-bit mixer (splitmix64 finalizer); the low 16 bits are the SR
+// dither.  Restated bit-for-bit in oracle/adamw_oracle.py (sr_bits).
+__device__ __forceinline__ uint32_t sr_bits(uint64_t seed, uint64_t idx) {
+  uint64_t x = seed ^ (idx * 0x9E3779B97F4A7C15ull);
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x & 0xFFFFull);
+}
+
+// one element of the bf16 path (p, g, m, v all bf16 in HBM)
+__device__ __forceinline__ void adamw_elem_bf16(float& p, float g, float& m, float& v,
+                                                const AdamwGroup& G, float coef, bool clip,
+                                                bool sr, uint64_t seed, uint64_t idx) {
+  if (clip) g = rbf(g * coef);                         // torch._foreach_mul_(grads, clip_coef)
+  p = rbf(p * G.wd_factor);                            // p.mul_(1 - lr*wd)
+  m = rbf(fmaf(G.one_minus_beta1, g - m, m));          // exp_avg.lerp_(grad, 1-beta1)
+  v = rbf(v * G.beta2);                                // exp_avg_sq.mul_(beta2)
+  v = rbf(fmaf(G.one_minus_beta2 * g, g, v));          //   .addcmul_(grad, grad, 1-beta2)
+  float d = rbf(sqrtf(v));                             // exp_avg_sq.sqrt()
+  d = rbf(d / G.bc2_sqrt);                             //   / bias_correction2_sqrt
+  d = rbf(d + G.eps);                                  //   .add_(eps)
+  const float r = p + (G.neg_step_size * m) / d;       // fp32 addcdiv on the fp32 copy
+  if (sr) {                                            // copy_stochastic_
+    uint32_t u = __float_as_uint(r);
+    u = (u + sr_bits(seed, idx)) & 0xFFFF0000u;
+    p = __uint_as_float(u);
+  } else {
+    p = rbf(r);                                        // p.addcdiv_ on bf16 p
+  }
+}
+
+__device__ __forceinline__ int find_group(const AdamwGroups& G, long long e) {
+  int gi = 0;
+#pragma unroll
+  for (int i = 1; i < ADAMW_MAX_GROUPS; ++i)
+    if (i < G.n && e >= G.g[i].begin) gi = i;
+  return gi;
+}
+
+// flat bf16 store; n multiple of 8 (the store pads every tensor to 8 elements)
+__global__ void __launch_bounds__(256) adamw_bf16_kernel(bf16_t* __restrict__ P, const bf16_t* __restrict__ Gr,
+                                                         bf16_t* __restrict__ M, bf16_t* __restrict__ V, long long n8,
+                                                         AdamwGroups groups, const float* __restrict__ clip_coef,
+                                                         int sr, unsigned long long seed) {
+  const bool clip = clip_coef != nullptr;
+  const float coef = clip ? clip_coef[0] : 1.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const long long e0 = i * 8;
+    const int gi = find_group(groups, e0);
+    const AdamwGroup& G = groups.g[gi];
+    if (e0 >= G.end) continue;  // padding tail beyond the last group
+    bf8 pv = reinterpret_cast<const bf8*>(P)[i];
+    bf8 gv = reinterpret_cast<const bf8*>(Gr)[i];
+    bf8 mv = reinterpret_cast<const bf8*>(M)[i];
+    bf8 vv = reinterpret_cast<const bf8*>(V)[i];
+    float p[8], g[8], m[8], v[8];
+    unpack8(pv, p); unpack8(gv, g); unpack8(mv, m); unpack8(vv, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adamw_elem_bf16(p[j], g[j], m[j], v[j], G, coef, clip, sr != 0, seed, (uint64_t)(e0 + j));
+    reinterpret_cast<bf8*>(P)[i] = pack8(p);
+    reinterpret_cast<bf8*>(M)[i] = pack8(m);
+    reinterpret_cast<bf8*>(V)[i] = pack8(v);
+  }
+}
+
+// fp32 store (LoRA weights are fp32 by default, TrainConfig.py:959): plain fp32 torch ops
+__global__ void __launch_bounds__(256) adamw_f32_kernel(float* __restrict__ P, const float* __restrict__ Gr,
+                                                        float* __restrict__ M, float* __restrict__ V, long long n4,
+                                                        AdamwGroups groups, const float* __restrict__ clip_coef) {
+  const bool clip = clip_coef != nullptr;
+  const float coef = clip ? clip_coef[0] : 1.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const long long e0 = i * 4;
+    const int gi = find_group(groups, e0);
+    const AdamwGroup& G = groups.g[gi];
+    if (e0 >= G.end) continue;
+    float4 pv = reinterpret_cast<const float4*>(P)[i];
+    float4 gv = reinterpret_cast<const float4*>(Gr)[i];
+    float4 mv = reinterpret_cast<const float4*>(M)[i];
+    float4 vv = reinterpret_cast<const float4*>(V)[i];
+    float* p = &pv.x; float* g = &gv.x; float* m = &mv.x; float* v = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gg = clip ? g[j] * coef : g[j];
+      p[j] = p[j] * G.wd_factor;
+      m[j] = fmaf(G.one_minus_beta1, gg - m[j], m[j]);
+      v[j] = v[j] * G.beta2;
+      v[j] = fmaf(G.one_minus_beta2 * gg, gg, v[j]);
+      float d = sqrtf(v[j]) / G.bc2_sqrt + G.eps;
+      p[j] = p[j] + (G.neg_step_size * m[j]) / d;
+    }
+    reinterpret_cast<float4*>(P)[i] = pv;
+    reinterpret_cast<float4*>(M)[i] = mv;
+    reinterpret_cast<float4*>(V)[i] = vv;
+  }
+}
+
+// ---- global grad norm ---------------------------------------------------------
+// chunk table: for each block, (tensor index, element begin, element end) in the flat store
+struct NormChunk { long long begin, end; int tensor; int pad; };
+
+template <typename T>
+__device__ __forceinline__ float ld_as_f(const T* p, long long i);
+template <> __device__ __forceinline__ float ld_as_f<bf16_t>(const bf16_t* p, long long i) { return bf2f(p[i]); }
+template <> __device__ __forceinline__ float ld_as_f<float>(const float* p, long long i) { return p[i]; }
+
+template <typename T>
+__global__ void __launch_bounds__(256) grad_sqnorm_kernel(const T* __restrict__ G, const NormChunk* __restrict__ chunks,
+                                                          double* __restrict__ tensor_sq) {
+  const NormChunk c = chunks[blockIdx.x];
+  double acc = 0.0;
+  // 16-byte vector body (chunk bounds are multiples of 8 elements)
+  for (long long e = c.begin + threadIdx.x * 8; e < c.end; e += 256 * 8) {
+    if (sizeof(T) == 2) {
+      bf8 v = *reinterpret_cast<const bf8*>(G + e);
+      float f[8];
+      unpack8(v, f);
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = fmaf(f[j], f[j], s);
+      acc += s;
+    } else {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { float f = ld_as_f<T>(G, e + j); s = fmaf(f, f, s); }
+      acc += s;
+    }
+  }
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&tensor_sq[c.tensor], red[0] + red[1] + red[2] + red[3]);
+}
+
+// total_norm / clip coefficient with torch's bf16 result dtypes:
+//   per-tensor norm (bf16) -> stack -> vector_norm (bf16) -> max_norm/(norm+1e-6) (bf16) -> clamp(max=1)
+// out[0] = clip coefficient (as float of a bf16 / f32 value), out[1] = total norm
+__global__ void clip_coef_kernel(const double* __restrict__ tensor_sq, int n_tensors, float max_norm, int bf16_grads,
+                                 float* __restrict__ out) {
+  __shared__ float red[16];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n_tensors; i += blockDim.x) {
+    float nrm = (float)sqrt(tensor_sq[i]);
+    if (bf16_grads) nrm = rbf(nrm);
+    acc = fmaf(nrm, nrm, acc);
+  }
+  const float tot_sq = block_sum(acc, red);
+  if (threadIdx.x == 0) {
+    float total = sqrtf(tot_sq);
+    float coef;
+    if (bf16_grads) {
+      total = rbf(total);
+      const float denom = rbf(total + 1e-6f);
+      coef = rbf(max_norm / denom);
+      coef = fminf(coef, 1.f);
+    } else {
+      coef = fminf(max_norm / (total + 1e-6f), 1.f);
+    }
+    out[0] = coef;
+    out[1] = total;
+  }
+}
+
+// ---- C ABI ----------------------------------------------------------------------
+static int adamw_grid(long long nvec) {
+  long long blocks = (nvec + 255) / 256;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+OTAMD_API int otamd_adamw_bf16(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups,
+                               int n_groups, const float* clip_coef, int stochastic_rounding,
+                               unsigned long long seed, hipStream_t stream) {
+  if (!p || !g || !m || !v || n < 0 || (n % 8) != 0 || n_groups < 1 || n_groups > ADAMW_MAX_GROUPS) return OTAMD_EINVAL;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  AdamwGroups G = {};
+  for (int i = 0; i < n_groups; ++i) G.g[i] = groups[i];
+  G.n = n_groups;
+  adamw_bf16_kernel<<<adamw_grid(n / 8), 256, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v,
+                                                           n / 8, G, clip_coef, stochastic_rounding, seed);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
+OTAMD_API int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups,
+                              int n_groups, const float* clip_coef, hipStream_t stream) {
+  if (!p || !g || !m || !v || n < 0 || (n % 4) != 0 || n_groups < 1 || n_groups > ADAMW_MAX_GROUPS) return OTAMD_EINVAL;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  AdamwGroups G = {};
+  for (int i = 0; i < n_groups; ++i) G.g[i] = groups[i];
+  G.n = n_groups;
+  adamw_f32_kernel<<<adamw_grid(n / 4), 256, 0, stream>>>((float*)p, (const float*)g, (float*)m, (float*)v, n / 4, G,
+                                                          clip_coef);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
+// grads: flat store (bf16 if grad_dtype==0 else f32); chunks: device table of n_chunks NormChunk;
+// tensor_sq: device double[n_tensors] (zeroed here); out: device float[2] = {clip coef, total norm}
+OTAMD_API int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void* chunks, int n_chunks,
+                                   double* tensor_sq, int n_tensors, float max_norm, float* out, hipStream_t stream) {
+  if (!grads || !chunks || !tensor_sq || !out || n_chunks < 0 || n_tensors < 1) return OTAMD_EINVAL;
+  if (hipMemsetAsync(tensor_sq, 0, sizeof(double) * n_tensors, stream) != hipSuccess) return OTAMD_ELAUNCH;
+  if (n_chunks > 0) {
+    if (grad_dtype == 0)
+      grad_sqnorm_kernel<bf16_t><<<n_chunks, 256, 0, stream>>>((const bf16_t*)grads, (const NormChunk*)chunks, tensor_sq);
+    else
+      grad_sqnorm_kernel<float><<<n_chunks, 256, 0, stream>>>((const float*)grads, (const NormChunk*)chunks, tensor_sq);
+    OTAMD_CHECK_LAUNCH();
+  }
+  clip_coef_kernel<<<1, 1024, 0, stream>>>(tensor_sq, n_tensors, max_norm, grad_dtype == 0, out);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
+// scale a flat grad store by the device clip coefficient (used when the optimizer is
+// not the fused AdamW, e.g. parity checks of clip_grad_norm_ alone)
+__global__ void scale_bf16_kernel(bf16_t* __restrict__ g, long long n8, const float* __restrict__ coef) {
+  const float c = coef[0];
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    bf8 v = reinterpret_cast<bf8*>(g)[i];
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * c;
+    reinterpret_cast<bf8*>(g)[i] = pack8(f);
+  }
+}
+OTAMD_API int otamd_scale_bf16_by_device_scalar(void* g, long long n, const float* coef, hipStream_t stream) {
+  if (!g || !coef || (n % 8) != 0 || ((uintptr_t)g & 15)) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  scale_bf16_kernel<<<adamw_grid(n / 8), 256, 0, stream>>>((bf16_t*)g, n / 8, coef);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}

@@ -1,0 +1,428 @@
+// bf16 MFMA GEMM engine for gfx950 (v_mfma_f32_16x16x32_bf16, fp32 accumulate).
+//
+// One kernel template covers every GEMM-shaped op of the UNet hot path
+// (SURVEY.md §2.3 rows conv3x3 / Linear GEMM; reference call sites
+// modules/modelSetup/BaseStableDiffusionXLSetup.py:268-273 -> diffusers UNet):
+//   Linear fwd   Y = X W^T          A: OPM_K (X [M,K])     B: OPM_K  (W [N,K])
+//   Linear dgrad dX = dY W          A: OPM_K (dY [M,N])    B: OPM_MN (W [N,K] read as [K'=N][N'=K])
+//   Linear wgrad dW = dY^T X        A: OPM_MN (dY)         B: OPM_MN (X)         (split-K slabs)
+//   conv fwd     implicit GEMM      A: OPM_CONV_FWD gather B: OPM_K (W [Cout][kh][kw][Cin])
+//   conv dgrad   transposed gather  A: OPM_CONV_DGRAD      B: OPM_K (W^T [Cin][kh][kw][Cout])
+//   conv wgrad   dW = dY^T im2col   A: OPM_MN (dY)         B: OPM_CONV_WGRAD gather
+// Activations are NHWC bf16, so a conv's rows are pixels and a Linear over tokens
+// reads the same tensor with no permute.
+//
+// Operand tiles are staged global -> registers -> LDS "as they lie" (16-byte chunks
+// along the contiguous dimension).  K-contiguous tiles are read with ds_read_b128,
+// MN-contiguous tiles with ds_read_b64_tr_b16 (hardware transpose), both XOR-swizzled
+// to be bank-conflict free.  The MFMA is issued with swapped operands (B-fragment as
+// the MFMA A operand) so each lane ends with 4 consecutive output columns.
+#include "common.h"
+
+enum { OPM_K = 0, OPM_MN = 1, OPM_CONV_FWD = 2, OPM_CONV_DGRAD = 3, OPM_CONV_WGRAD = 4 };
+
+struct ConvGeom {
+  int N;             // batch
+  int SH, SW, SC;    // gathered (source) tensor: spatial dims and channel count
+  int RH, RW;        // spatial dims decoding a GEMM row index (fwd: output, dgrad: input, wgrad: output)
+  int KH, KW, stride, pad;
+  int upsample;      // source read through a virtual nearest-2x upsample (fwd / wgrad)
+  int pad_;
+  long long ld;      // pixel stride of the source, elements
+};
+
+struct GemmArgs {
+  const bf16_t* A; long long lda; int amode;
+  const bf16_t* B; long long ldb; int bmode;
+  void* C; long long ldc; int c_f32; int accumulate;
+  int M, N, K;
+  float alpha;
+  const bf16_t* bias;                                          // + bias[n]
+  const bf16_t* rowvec; long long ldv; int rows_per_vec;       // + rowvec[(m/rows_per_vec)*ldv + n]
+  const bf16_t* residual; long long ldr;                       // + residual[m*ldr + n]
+  float* slab;                                                 // split-K partials [splits][M][N]
+  int k_per_split;
+  ConvGeom ga, gb;
+};
+
+#define BM 128
+#define BN 128
+#define BK 64
+#define NTHREADS 256
+
+// --- LDS images ------------------------------------------------------------------------
+// K-mode image: [BMN rows][64 k], 128-byte rows, 16-byte chunk c stored at c ^ (row & 7)
+__device__ __forceinline__ int kimg_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// MN-mode image: [64 k rows][128 mn], 256-byte rows, 32-byte block b stored at b ^ s(k)
+__device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+__device__ __forceinline__ int mnimg_off(int k, int col) {  // col: element index, multiple of 4
+  const int blk = col >> 4, within = (col & 15) << 1;
+  return k * 256 + ((blk ^ mn_swz(k)) << 5) + within;
+}
+
+// --- global gathers ----------------------------------------------------------------------
+__device__ __forceinline__ bf8 zero8() { bf8 z; z.w[0] = z.w[1] = z.w[2] = z.w[3] = 0; return z; }
+__device__ __forceinline__ bf8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf8*>(p); }
+
+// per-thread cached row decode for K-mode gathers (4 rows per thread)
+struct RowCtx { int n[4], y0[4], x0[4]; bool ok[4]; };
+
+template <int MODE>
+__device__ __forceinline__ void kmode_prepare(const ConvGeom& g, int mn0, int MNsz, RowCtx& rc) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = mn0 + (tid >> 3) + 32 * i;
+    rc.ok[i] = row < MNsz;
+    if (MODE == OPM_CONV_FWD || MODE == OPM_CONV_DGRAD) {
+      const int rr = rc.ok[i] ? row : 0;
+      const int hw = g.RH * g.RW;
+      const int n = rr / hw, rem = rr - n * hw;
+      const int y = rem / g.RW, x = rem - y * g.RW;
+      rc.n[i] = n;
+      if (MODE == OPM_CONV_FWD) { rc.y0[i] = y * g.stride - g.pad; rc.x0[i] = x * g.stride - g.pad; }
+      else { rc.y0[i] = y + g.pad; rc.x0[i] = x + g.pad; }
+    }
+  }
+}
+
+// load this thread's 4 chunks of a K-mode tile (rows mn0.., k chunk k0 + 8*(tid&7))
+template <int MODE>
+__device__ __forceinline__ void kmode_load(const bf16_t* __restrict__ X, long long ld, const ConvGeom& g, int mn0,
+                                           int k0, int K, const RowCtx& rc, bf8 (&st)[4]) {
+  const int tid = threadIdx.x;
+  const int k = k0 + 8 * (tid & 7);
+  const bool kok = k < K;
+  if (MODE == OPM_K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = mn0 + (tid >> 3) + 32 * i;
+      st[i] = (kok && rc.ok[i]) ? ld8(X + (long long)row * ld + k) : zero8();
+    }
+  } else {
+    const int tap = kok ? k / g.SC : 0;
+    const int ch = k - tap * g.SC;
+    const int r = tap / g.KW, s = tap - r * g.KW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool ok = kok && rc.ok[i];
+      int sy, sx;
+      if (MODE == OPM_CONV_FWD) {
+        const int y = rc.y0[i] + r, x = rc.x0[i] + s;
+        if (g.upsample) {
+          ok = ok && y >= 0 && y < 2 * g.SH && x >= 0 && x < 2 * g.SW;
+          sy = y >> 1; sx = x >> 1;
+        } else {
+          ok = ok && y >= 0 && y < g.SH && x >= 0 && x < g.SW;
+          sy = y; sx = x;
+        }
+      } else {  // dgrad: source pixel ((h+pad-r)/st, (w+pad-s)/st) when divisible
+        const int ty = rc.y0[i] - r, tx = rc.x0[i] - s;
+        if (g.stride == 1) { sy = ty; sx = tx; }
+        else {
+          ok = ok && ty >= 0 && tx >= 0 && (ty % g.stride) == 0 && (tx % g.stride) == 0;
+          sy = ty / g.stride; sx = tx / g.stride;
+        }
+        ok = ok && sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW;
+      }
+      st[i] = ok ? ld8(X + ((long long)(rc.n[i] * g.SH + sy) * g.SW + sx) * g.ld + ch) : zero8();
+    }
+  }
+}
+
+__device__ __forceinline__ void kmode_store(char* img, const bf8 (&st)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (tid >> 3) + 32 * i;
+    *reinterpret_cast<bf8*>(img + kimg_off(row, tid & 7)) = st[i];
+  }
+}
+
+// MN-mode: this thread's 4 chunks are (k rows tid/16 + 16 i, mn chunk 8*(tid&15))
+struct ColCtx { int r, s, ch; bool ok; };
+
+template <int MODE>
+__device__ __forceinline__ void mnmode_prepare(const ConvGeom& g, int mn0, int MNsz, ColCtx& cc) {
+  const int col = mn0 + 8 * (threadIdx.x & 15);
+  cc.ok = col < MNsz;
+  if (MODE == OPM_CONV_WGRAD) {
+    const int c = cc.ok ? col : 0;
+    const int tap = c / g.SC;
+    cc.ch = c - tap * g.SC;
+    cc.r = tap / g.KW;
+    cc.s = tap - cc.r * g.KW;
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void mnmode_load(const bf16_t* __restrict__ X, long long ld, const ConvGeom& g, int mn0,
+                                            int k0, int K, const ColCtx& cc, bf8 (&st)[4]) {
+  const int tid = threadIdx.x;
+  const int col = mn0 + 8 * (tid & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + (tid >> 4) + 16 * i;
+    bool ok = cc.ok && k < K;
+    if (MODE == OPM_MN) {
+      st[i] = ok ? ld8(X + (long long)k * ld + col) : zero8();
+    } else {  // OPM_CONV_WGRAD: k = output pixel, col = (r, s, ch)
+      const int kk = ok ? k : 0;
+      const int hw = g.RH * g.RW;
+      const int n = kk / hw, rem = kk - n * hw;
+      const int p = rem / g.RW, q = rem - p * g.RW;
+      const int y = p * g.stride - g.pad + cc.r, x = q * g.stride - g.pad + cc.s;
+      int sy, sx;
+      if (g.upsample) { ok = ok && y >= 0 && y < 2 * g.SH && x >= 0 && x < 2 * g.SW; sy = y >> 1; sx = x >> 1; }
+      else { ok = ok && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
+      st[i] = ok ? ld8(X + ((long long)(n * g.SH + sy) * g.SW + sx) * g.ld + cc.ch) : zero8();
+    }
+  }
+}
+
+__device__ __forceinline__ void mnmode_store(char* img, const bf8 (&st)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = (tid >> 4) + 16 * i;
+    const int col = 8 * (tid & 15);
+    *reinterpret_cast<bf8*>(img + mnimg_off(k, col)) = st[i];   // 16 B stay inside one 32-B block
+  }
+}
+
+// --- fragment reads --------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) short4v lds_short4;
+
+__device__ __forceinline__ bf16x8 frag_k(const char* img, int mnb, int kb) {
+  const int lane = threadIdx.x & 63;
+  const int row = mnb + (lane & 15);
+  const int chunk = (kb >> 3) + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(img + kimg_off(row, chunk));
+}
+__device__ __forceinline__ bf16x8 frag_mn(const char* img, int mnb, int kb) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k0 = kb + 8 * g + q;
+  const int col = mnb + 4 * p;
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(img + mnimg_off(k0, col)));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(img + mnimg_off(k0 + 4, col)));
+  short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int MODE> struct IsK { static constexpr bool v = (MODE == OPM_K || MODE == OPM_CONV_FWD || MODE == OPM_CONV_DGRAD); };
+
+// XCD-aware bijective remap of a linear workgroup id (cdna_hip_programming.md §5 T1)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+template <int AM, int BMODE>
+__global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs args) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tm = wg % tiles_m, tn = wg / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * args.k_per_split;
+  const int kend = min(args.K, kbeg + args.k_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+
+  RowCtx rcA, rcB;
+  ColCtx ccA, ccB;
+  constexpr bool AK = IsK<AM>::v, BKm = IsK<BMODE>::v;
+  if (AK) kmode_prepare<AM>(args.ga, m0, args.M, rcA); else mnmode_prepare<AM>(args.ga, m0, args.M, ccA);
+  if (BKm) kmode_prepare<BMODE>(args.gb, n0, args.N, rcB); else mnmode_prepare<BMODE>(args.gb, n0, args.N, ccB);
+
+  bf8 sa[4], sb[4];
+  auto load_tiles = [&](int k0) {
+    if (AK) kmode_load<AM>(args.A, args.lda, args.ga, m0, k0, kend, rcA, sa);
+    else mnmode_load<AM>(args.A, args.lda, args.ga, m0, k0, kend, ccA, sa);
+    if (BKm) kmode_load<BMODE>(args.B, args.ldb, args.gb, n0, k0, kend, rcB, sb);
+    else mnmode_load<BMODE>(args.B, args.ldb, args.gb, n0, k0, kend, ccB, sb);
+  };
+  auto store_tiles = [&](int buf) {
+    char* imA = smem + buf * 16384;
+    char* imB = smem + 32768 + buf * 16384;
+    if (AK) kmode_store(imA, sa); else mnmode_store(imA, sa);
+    if (BKm) kmode_store(imB, sb); else mnmode_store(imB, sb);
+  };
+
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;   // 2 x 2 waves, 64 x 64 each
+  float4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load_tiles(kbeg);
+    store_tiles(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+    const char* ia = smem + cur * 16384;
+    const char* ib = smem + 32768 + cur * 16384;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = AK ? frag_k(ia, wm * 64 + i * 16, kk) : frag_mn(ia, wm * 64 + i * 16, kk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = BKm ? frag_k(ib, wn * 64 + j * 16, kk) : frag_mn(ib, wn * 64 + j * 16, kk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[m][n..n+3], m = ... + (lane&15), n = ... + 4*(lane>>4)
+  const int lane = threadIdx.x & 63;
+  const bool use_slab = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= args.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= args.N) continue;   // N % 4 == 0 is a launcher precondition
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (use_slab) {
+        float* dst = args.slab + ((long long)split * args.M + m) * args.N + n;
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        continue;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] *= args.alpha;
+      if (args.bias) {
+        const uint2 b = *reinterpret_cast<const uint2*>(args.bias + n);
+        v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+        v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+      }
+      if (args.rowvec) {
+        const uint2 b = *reinterpret_cast<const uint2*>(args.rowvec + (long long)(m / args.rows_per_vec) * args.ldv + n);
+        v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+        v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+      }
+      if (args.residual) {
+        const uint2 b = *reinterpret_cast<const uint2*>(args.residual + (long long)m * args.ldr + n);
+        v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+        v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+      }
+      if (args.c_f32) {
+        float* dst = reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n;
+        if (args.accumulate) { float4 o = *reinterpret_cast<float4*>(dst); v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w; }
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
+        if (args.accumulate) {
+          const uint2 o = *reinterpret_cast<const uint2*>(dst);
+          v[0] += __uint_as_float(o.x << 16); v[1] += __uint_as_float(o.x & 0xffff0000u);
+          v[2] += __uint_as_float(o.y << 16); v[3] += __uint_as_float(o.y & 0xffff0000u);
+        }
+        uint2 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(dst) = o;
+      }
+    }
+  }
+}
+
+// split-K reduction + the same epilogue: C = alpha * sum_s slab[s] (+bias, +rowvec, +residual) (+C if accumulate)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs args, int splits) {
+  const long long total4 = (long long)args.M * args.N / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total4; i += (long long)gridDim.x * blockDim.x) {
+    const long long e = i * 4;
+    const int m = (int)(e / args.N), n = (int)(e - (long long)m * args.N);
+    float4 s = *reinterpret_cast<const float4*>(args.slab + e);
+    for (int z = 1; z < splits; ++z) {
+      const float4 t = *reinterpret_cast<const float4*>(args.slab + (long long)z * args.M * args.N + e);
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    float v[4] = {s.x * args.alpha, s.y * args.alpha, s.z * args.alpha, s.w * args.alpha};
+    if (args.bias) for (int t = 0; t < 4; ++t) v[t] += bf2f(args.bias[n + t]);
+    if (args.rowvec) for (int t = 0; t < 4; ++t) v[t] += bf2f(args.rowvec[(long long)(m / args.rows_per_vec) * args.ldv + n + t]);
+    if (args.residual) for (int t = 0; t < 4; ++t) v[t] += bf2f(args.residual[(long long)m * args.ldr + n + t]);
+    if (args.c_f32) {
+      float* dst = reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n;
+      for (int t = 0; t < 4; ++t) dst[t] = args.accumulate ? dst[t] + v[t] : v[t];
+    } else {
+      bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
+      for (int t = 0; t < 4; ++t) dst[t] = f2bf(args.accumulate ? bf2f(dst[t]) + v[t] : v[t]);
+    }
+  }
+}
+
+typedef void (*gemm_fn)(GemmArgs);
+
+static gemm_fn pick(int am, int bm) {
+#define CASE(a, b) if (am == a && bm == b) return gemm_kernel<a, b>;
+  CASE(OPM_K, OPM_K)
+  CASE(OPM_K, OPM_MN)
+  CASE(OPM_MN, OPM_MN)
+  CASE(OPM_MN, OPM_K)
+  CASE(OPM_CONV_FWD, OPM_K)
+  CASE(OPM_CONV_DGRAD, OPM_K)
+  CASE(OPM_MN, OPM_CONV_WGRAD)
+#undef CASE
+  return nullptr;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// C-ABI.  Preconditions (checked, OTAMD_EINVAL otherwise): M,N,K > 0; N % 4 == 0; K-mode
+// operands need K % 8 == 0, MN-mode operands MN % 8 == 0; leading dims multiples of 8
+// elements; base pointers 16-byte aligned; conv gathers need SC % 8 == 0.
+// workspace: >= splits * M * N * 4 bytes when splits > 1.
+OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_bytes, hipStream_t stream) {
+  if (!in) return OTAMD_EINVAL;
+  GemmArgs a = *in;
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 1) return OTAMD_EINVAL;
+  if (!a.A || !a.B || !a.C || !aligned16(a.A) || !aligned16(a.B)) return OTAMD_EINVAL;
+  gemm_fn fn = pick(a.amode, a.bmode);
+  if (!fn) return OTAMD_EUNSUPPORTED;
+  const bool ak = (a.amode != OPM_MN), bk = (a.bmode == OPM_K);
+  if (ak && (a.K % 8)) return OTAMD_EINVAL;
+  if (!ak && (a.M % 8)) return OTAMD_EINVAL;
+  if (bk && (a.K % 8)) return OTAMD_EINVAL;
+  if (!bk && (a.N % 8)) return OTAMD_EINVAL;
+  if ((a.lda % 8) || (a.ldb % 8) || (a.ldc % 4)) return OTAMD_EINVAL;
+  if (a.amode >= OPM_CONV_FWD && ((a.ga.SC % 8) || (a.ga.ld % 8))) return OTAMD_EINVAL;
+  if (a.bmode >= OPM_CONV_FWD && ((a.gb.SC % 8) || (a.gb.ld % 8))) return OTAMD_EINVAL;
+  if (a.rowvec && a.rows_per_vec <= 0) return OTAMD_EINVAL;
+  long long kps = ((long long)(a.K + splits - 1) / splits + BK - 1) / BK * BK;
+  splits = (int)((a.K + kps - 1) / kps);
+  a.k_per_split = (int)kps;
+  if (splits > 1) {
+    if (!workspace || ws_bytes < (long long)splits * a.M * a.N * 4 || !aligned16(workspace)) return OTAMD_EINVAL;
+    a.slab = (float*)workspace;
+  } else {
+    a.slab = nullptr;
+  }
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, 1, splits);
+  hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);
+  OTAMD_CHECK_LAUNCH();
+  if (splits > 1) {
+    long long t4 = (long long)a.M * a.N / 4;
+    int blocks = (int)std::min<long long>((t4 + 255) / 256, 4096);
+    splitk_reduce_kernel<<<blocks, 256, 0, stream>>>(a, splits);
+    OTAMD_CHECK_LAUNCH();
+  }
+  return OTAMD_OK;
+}
+
+OTAMD_API int otamd_gemm_args_size(void) { return (int)sizeof(GemmArgs); }
+OTAMD_API int otamd_conv_geom_size(void) { return (int)sizeof(ConvGeom); }

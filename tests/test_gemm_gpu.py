@@ -1,0 +1,94 @@
+"""GEMM engine parity vs a plain PyTorch fp32 reference of the same op (GPU)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from onetrainer_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def rnd(*s, dev, scale=1.0):
+    return (torch.randn(*s, device=dev) * scale).to(BF)
+
+
+def close(out, ref, tol=2e-2):
+    out = out.float()
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err / scale < tol, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("M,N,Kd", [(128, 128, 64), (256, 384, 320), (77, 640, 2048), (4100, 1280, 640), (8, 1280, 320)])
+def test_linear_fwd(dev, M, N, Kd):
+    torch.manual_seed(0)
+    x, w = rnd(M, Kd, dev=dev), rnd(N, Kd, dev=dev, scale=0.05)
+    b, r = rnd(N, dev=dev), rnd(M, N, dev=dev)
+    y = K.linear(x, w, bias=b, residual=r)
+    ref = x.float() @ w.float().t() + b.float() + r.float()
+    close(y, ref)
+
+
+def test_linear_asymmetric_exact(dev):
+    # integer-valued operands: exact in bf16/fp32, catches any transposed fragment map
+    torch.manual_seed(1)
+    M, N, Kd = 256, 256, 128
+    x = torch.randint(-3, 4, (M, Kd), device=dev).to(BF)
+    w = torch.randint(-3, 4, (N, Kd), device=dev).to(BF)
+    y = K.linear(x, w, out_dtype=torch.float32)
+    assert torch.equal(y, x.float() @ w.float().t())
+    dy = torch.randint(-2, 3, (M, N), device=dev).to(BF)
+    dx = K.linear_dgrad(dy, w, out=torch.empty(M, Kd, device=dev, dtype=torch.float32))
+    assert torch.equal(dx, dy.float() @ w.float())
+    dw = K.linear_wgrad(dy, x, out=torch.empty(N, Kd, device=dev, dtype=torch.float32))
+    assert torch.equal(dw, dy.float().t() @ x.float())
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 640, 640), (4096, 640, 5120), (300, 2048, 640)])
+def test_linear_dgrad(dev, M, N, Kd):
+    torch.manual_seed(2)
+    dy, w = rnd(M, N, dev=dev), rnd(N, Kd, dev=dev, scale=0.05)
+    dx = K.linear_dgrad(dy, w)
+    close(dx, dy.float() @ w.float())
+
+
+@pytest.mark.parametrize("T,N,Kd", [(4096, 640, 640), (16384, 1280, 1280), (312, 640, 2048), (8, 1280, 2816)])
+def test_linear_wgrad(dev, T, N, Kd):
+    torch.manual_seed(3)
+    dy, x = rnd(T, N, dev=dev), rnd(T, Kd, dev=dev)
+    dw = K.linear_wgrad(dy, x, out=torch.empty(N, Kd, device=dev, dtype=torch.float32))
+    close(dw, dy.float().t() @ x.float(), tol=1e-2)
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).float()
+
+
+def to_nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,stride,up", [
+    (2, 16, 16, 64, 128, 1, False), (2, 32, 24, 320, 320, 1, False), (1, 16, 16, 128, 64, 2, False),
+    (2, 8, 8, 128, 128, 1, True), (1, 64, 64, 8, 320, 1, False)])
+def test_conv_fwd_dgrad_wgrad(dev, N, H, W, Cin, Cout, stride, up):
+    torch.manual_seed(4)
+    x = rnd(N, H, W, Cin, dev=dev)
+    w = rnd(Cout, 3, 3, Cin, dev=dev, scale=0.05)
+    b = rnd(Cout, dev=dev)
+    y = K.conv2d(x, w, bias=b, stride=stride, pad=1, upsample=up)
+    xr = nchw(x).requires_grad_(True)
+    xin = F.interpolate(xr, scale_factor=2.0, mode="nearest") if up else xr
+    wr = w.permute(0, 3, 1, 2).float().requires_grad_(True)
+    ref = F.conv2d(xin, wr, b.float(), stride=stride, padding=1)
+    close(y, to_nhwc(ref))
+    dy = rnd(*y.shape, dev=dev)
+    ref.backward(nchw(dy))
+    dw = K.conv2d_wgrad(dy, x, 3, stride, 1, upsample=up, out=torch.empty_like(w, dtype=torch.float32))
+    close(dw, wr.grad.permute(0, 2, 3, 1), tol=1e-2)
+    if not up:
+        wt = w.permute(3, 1, 2, 0).contiguous()
+        dx = K.conv2d_dgrad(dy, wt, (H, W), stride, 1)
+        close(dx, to_nhwc(xr.grad))
