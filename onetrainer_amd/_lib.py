@@ -42,7 +42,20 @@ class NormChunk(C.Structure):
     _fields_ = [("begin", C.c_longlong), ("end", C.c_longlong), ("tensor", C.c_int), ("pad", C.c_int)]
 
 
+class AttnArgs(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("k", C.c_void_p), ("v", C.c_void_p), ("o", C.c_void_p), ("lse", C.c_void_p),
+                ("dout", C.c_void_p), ("delta", C.c_void_p), ("dq", C.c_void_p), ("dk", C.c_void_p),
+                ("dv", C.c_void_p), ("dk32", C.c_void_p), ("dv32", C.c_void_p),
+                ("ldq", C.c_longlong), ("ldk", C.c_longlong), ("ldv", C.c_longlong), ("ldo", C.c_longlong),
+                ("lddo", C.c_longlong), ("lddq", C.c_longlong), ("lddk", C.c_longlong), ("lddv", C.c_longlong),
+                ("bsq", C.c_longlong), ("bsk", C.c_longlong), ("bsv", C.c_longlong), ("bso", C.c_longlong),
+                ("bsdo", C.c_longlong), ("bsdq", C.c_longlong), ("bsdk", C.c_longlong), ("bsdv", C.c_longlong),
+                ("B", C.c_int), ("H", C.c_int), ("Nq", C.c_int), ("Nk", C.c_int), ("Dv", C.c_int),
+                ("scale", C.c_float), ("qsplit", C.c_int), ("pad_", C.c_int)]
+
+
 VP, I, LL, F, D = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
+U64 = C.c_ulonglong
 
 # symbol -> argtypes (restype int).  Mirrors include/otamd.h one-for-one.
 SIGNATURES: dict[str, list] = {
@@ -53,6 +66,34 @@ SIGNATURES: dict[str, list] = {
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],
     "otamd_grad_clip_coef": [VP, I, VP, I, VP, I, F, VP, VP],
     "otamd_scale_bf16_by_device_scalar": [VP, LL, VP, VP],
+    # norm.hip
+    "otamd_groupnorm_fwd": [VP, LL, VP, LL, I, I, I, I, F, VP, VP, I, VP, VP, VP, VP, VP, VP],
+    "otamd_groupnorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, I, I, VP, I, VP, VP, VP, VP, VP, VP, VP, VP, I, VP],
+    "otamd_layernorm_fwd": [VP, LL, VP, LL, I, I, F, VP, VP, VP, VP, VP],
+    "otamd_layernorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, VP, I, VP],
+    # attention.hip
+    "otamd_attn_args_size": [],
+    "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],
+    "otamd_attn_bwd": [C.POINTER(AttnArgs), VP, LL, VP],
+    # elementwise.hip
+    "otamd_geglu_fwd": [VP, LL, VP, LL, I, I, VP],
+    "otamd_geglu_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP],
+    "otamd_silu_fwd": [VP, VP, LL, VP],
+    "otamd_silu_bwd": [VP, VP, VP, LL, VP],
+    "otamd_concat_channels": [VP, LL, I, VP, LL, I, VP, LL, VP],
+    "otamd_upsample2x_bwd": [VP, VP, I, I, I, I, I, VP],
+    "otamd_colsum": [VP, LL, I, I, I, VP, VP],
+    "otamd_conv_weight_transpose": [VP, VP, I, I, I, VP],
+    "otamd_cast_f32_bf16": [VP, VP, LL, VP],
+    "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
+    "otamd_add": [VP, VP, VP, LL, VP],
+    # diffusion.hip
+    "otamd_noise": [VP, I, LL, LL, U64, VP],
+    "otamd_timesteps": [VP, I, LL, U64, I, I, F, F, F, F, F, VP],
+    "otamd_ddpm_prologue": [VP, VP, I, VP, VP, VP, VP, F, I, LL, I, I, VP, VP, I, VP, VP],
+    "otamd_flow_prologue": [VP, VP, I, VP, F, F, I, I, LL, I, I, VP, VP, VP],
+    "otamd_mse_loss": [VP, I, VP, I, I, LL, I, F, F, VP, VP, VP, VP, I, F, I, F, VP, LL, VP, VP, VP, VP],
+    "otamd_mse_grad": [VP, I, VP, I, I, LL, I, VP, VP, VP, VP],
 }
 
 _lib = None
@@ -83,3 +124,4 @@ def check_layouts():
     L = lib()
     assert L.otamd_gemm_args_size() == C.sizeof(GemmArgs), (L.otamd_gemm_args_size(), C.sizeof(GemmArgs))
     assert L.otamd_conv_geom_size() == C.sizeof(ConvGeom)
+    assert L.otamd_attn_args_size() == C.sizeof(AttnArgs), (L.otamd_attn_args_size(), C.sizeof(AttnArgs))

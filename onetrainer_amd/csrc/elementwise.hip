@@ -1,0 +1,280 @@
+// HBM-bound helper kernels of the UNet step (all 16-byte vectorized, grid-stride):
+//   GEGLU fwd/bwd (diffusers GEGLU: hidden, gate = proj(x).chunk(2); hidden * gelu(gate)),
+//   SiLU fwd/bwd, channel concat (skip connections), nearest-2x upsample backward (2x2 sum),
+//   per-group column sums (bias / time-embedding grads), conv weight transposes,
+//   sinusoidal timestep embedding (diffusers get_timestep_embedding, flip_sin_to_cos=True,
+//   downscale_freq_shift=0), add.
+#include "common.h"
+
+static int grid_for(long long n) {
+  long long b = (n + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
+}
+#define GRID_STRIDE(i, n) for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); i += (long long)gridDim.x * blockDim.x)
+
+// h: [M, 2F] (hidden | gate), out: [M, F]
+__global__ void geglu_fwd_kernel(const bf16_t* __restrict__ h, long long ldh, bf16_t* __restrict__ out, long long ldo,
+                                 int M, int F) {
+  const int F8 = F >> 3;
+  GRID_STRIDE(i, (long long)M * F8) {
+    const long long m = i / F8;
+    const int c = (int)(i - m * F8) * 8;
+    float a[8], g[8];
+    unpack8(*reinterpret_cast<const bf8*>(h + m * ldh + c), a);
+    unpack8(*reinterpret_cast<const bf8*>(h + m * ldh + F + c), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = a[j] * gelu_f(g[j]);
+    *reinterpret_cast<bf8*>(out + m * ldo + c) = pack8(a);
+  }
+}
+__global__ void geglu_bwd_kernel(const bf16_t* __restrict__ h, long long ldh, const bf16_t* __restrict__ dout,
+                                 long long lddo, bf16_t* __restrict__ dh, long long lddh, int M, int F) {
+  const int F8 = F >> 3;
+  GRID_STRIDE(i, (long long)M * F8) {
+    const long long m = i / F8;
+    const int c = (int)(i - m * F8) * 8;
+    float a[8], g[8], d[8], da[8], dg[8];
+    unpack8(*reinterpret_cast<const bf8*>(h + m * ldh + c), a);
+    unpack8(*reinterpret_cast<const bf8*>(h + m * ldh + F + c), g);
+    unpack8(*reinterpret_cast<const bf8*>(dout + m * lddo + c), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      da[j] = d[j] * gelu_f(g[j]);
+      dg[j] = d[j] * a[j] * dgelu_f(g[j]);
+    }
+    *reinterpret_cast<bf8*>(dh + m * lddh + c) = pack8(da);
+    *reinterpret_cast<bf8*>(dh + m * lddh + F + c) = pack8(dg);
+  }
+}
+
+// elementwise SiLU on a dense bf16 buffer (n % 8 == 0)
+__global__ void silu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8) {
+  GRID_STRIDE(i, n8) {
+    float f[8];
+    unpack8(reinterpret_cast<const bf8*>(x)[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = silu_f(f[j]);
+    reinterpret_cast<bf8*>(y)[i] = pack8(f);
+  }
+}
+__global__ void silu_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+                                long long n8) {
+  GRID_STRIDE(i, n8) {
+    float f[8], g[8];
+    unpack8(reinterpret_cast<const bf8*>(x)[i], f);
+    unpack8(reinterpret_cast<const bf8*>(dy)[i], g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = g[j] * dsilu_f(f[j]);
+    reinterpret_cast<bf8*>(dx)[i] = pack8(g);
+  }
+}
+
+// out[p, 0:Ca] = a[p], out[p, Ca:Ca+Cb] = b[p]
+__global__ void concat_kernel(const bf16_t* __restrict__ a, long long lda, int Ca, const bf16_t* __restrict__ b,
+                              long long ldb, int Cb, bf16_t* __restrict__ out, long long P) {
+  const int C8 = (Ca + Cb) >> 3, A8 = Ca >> 3;
+  GRID_STRIDE(i, P * C8) {
+    const long long p = i / C8;
+    const int c8 = (int)(i - p * C8);
+    const bf8 v = c8 < A8 ? *reinterpret_cast<const bf8*>(a + p * lda + c8 * 8)
+                          : *reinterpret_cast<const bf8*>(b + p * ldb + (c8 - A8) * 8);
+    *reinterpret_cast<bf8*>(out + p * (Ca + Cb) + c8 * 8) = v;
+  }
+}
+
+// dx[n,h,w,c] = sum over the 2x2 block of dup[n,2h+i,2w+j,c]   (+ dx if accumulate)
+__global__ void upsample_bwd_kernel(const bf16_t* __restrict__ dup, bf16_t* __restrict__ dx, int N, int H, int W, int C,
+                                    int accumulate) {
+  const int C8 = C >> 3;
+  GRID_STRIDE(i, (long long)N * H * W * C8) {
+    const int c8 = (int)(i % C8);
+    long long t = i / C8;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H), n = (int)(t / H);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dxx = 0; dxx < 2; ++dxx) {
+        float f[8];
+        unpack8(*reinterpret_cast<const bf8*>(dup + (((long long)n * 2 * H + 2 * h + dy) * 2 * W + 2 * w + dxx) * C + c8 * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+    bf16_t* dst = dx + (((long long)n * H + h) * W + w) * C + c8 * 8;
+    if (accumulate) {
+      float f[8];
+      unpack8(*reinterpret_cast<const bf8*>(dst), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+    *reinterpret_cast<bf8*>(dst) = pack8(s);
+  }
+}
+
+// out[g, n] (fp32) = sum_{m in group g} x[m, n];  rows_per_group rows per group; grid (ceil(N/256)... )
+// block: 256 threads = 32 column-chunks(8 cols) x 8 row-lanes
+__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, long long ldx, int M, int N,
+                                                     int rows_per_group, int rows_per_block, float* __restrict__ out) {
+  __shared__ float red[8][256 + 8];
+  const int cchunk = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int col = (blockIdx.x * 32 + cchunk) * 8;
+  const int g = blockIdx.z;
+  const int r0 = g * rows_per_group + blockIdx.y * rows_per_block;
+  const int r1 = min(min(M, (g + 1) * rows_per_group), r0 + rows_per_block);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < N) {
+    for (int m = r0 + rl; m < r1; m += 8) {
+      float f[8];
+      unpack8(*reinterpret_cast<const bf8*>(x + (long long)m * ldx + col), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cchunk * 8 + j] = s[j];
+  __syncthreads();
+  if (rl == 0 && col < N) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
+      for (int k = 0; k < 8; ++k) t += red[k][cchunk * 8 + j];
+      atomicAdd(&out[(long long)g * N + col + j], t);
+    }
+  }
+}
+
+// w [Cout][KH][KW][Cin] -> wt [Cin][KH][KW][Cout]
+__global__ void conv_wt_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt, int Cout, int KK, int Cin) {
+  GRID_STRIDE(i, (long long)Cout * KK * Cin) {
+    const int ci = (int)(i % Cin);
+    long long t = i / Cin;
+    const int kk = (int)(t % KK), co = (int)(t / KK);
+    wt[((long long)ci * KK + kk) * Cout + co] = w[i];
+  }
+}
+
+// fp32 -> bf16 cast (n elements) and bf16 -> fp32
+__global__ void cast_f2b_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
+  GRID_STRIDE(i, n) y[i] = f2bf(x[i]);
+}
+
+// emb[b, :] = [cos(t*f_i), sin(t*f_i)], f_i = exp(-ln(10000) * i / half)   (flip_sin_to_cos=True, shift 0)
+// t is float32 (timesteps cast by .float() in diffusers); out bf16 row stride ldo
+__global__ void timestep_embedding_kernel(const float* __restrict__ t, int n, int dim, bf16_t* __restrict__ out,
+                                          long long ldo) {
+  const int half = dim / 2;
+  GRID_STRIDE(i, (long long)n * half) {
+    const int b = (int)(i / half), k = (int)(i - (long long)b * half);
+    // torch: exponent = -math.log(10000) * arange(half, f32) ; exponent / half ; exp(exponent)
+    const float expo = (-9.210340371976184f * (float)k) / (float)half;
+    const float f = expf(expo);
+    const float a = t[b] * f;
+    out[(long long)b * ldo + k] = f2bf(cosf(a));
+    out[(long long)b * ldo + half + k] = f2bf(sinf(a));
+  }
+}
+
+// y = a + b (dense bf16)
+__global__ void add_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ y, long long n8) {
+  GRID_STRIDE(i, n8) {
+    float fa[8], fb[8];
+    unpack8(reinterpret_cast<const bf8*>(a)[i], fa);
+    unpack8(reinterpret_cast<const bf8*>(b)[i], fb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fa[j] += fb[j];
+    reinterpret_cast<bf8*>(y)[i] = pack8(fa);
+  }
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+OTAMD_API int otamd_geglu_fwd(const void* h, long long ldh, void* out, long long ldo, int M, int F, hipStream_t s) {
+  if (!h || !out || M < 0 || F % 8 || ldh % 8 || ldo % 8 || !al16(h) || !al16(out)) return OTAMD_EINVAL;
+  if (M == 0) return OTAMD_OK;
+  geglu_fwd_kernel<<<grid_for((long long)M * F / 8), 256, 0, s>>>((const bf16_t*)h, ldh, (bf16_t*)out, ldo, M, F);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_geglu_bwd(const void* h, long long ldh, const void* dout, long long lddo, void* dh, long long lddh,
+                              int M, int F, hipStream_t s) {
+  if (!h || !dout || !dh || M < 0 || F % 8 || ldh % 8 || lddo % 8 || lddh % 8) return OTAMD_EINVAL;
+  if (!al16(h) || !al16(dout) || !al16(dh)) return OTAMD_EINVAL;
+  if (M == 0) return OTAMD_OK;
+  geglu_bwd_kernel<<<grid_for((long long)M * F / 8), 256, 0, s>>>((const bf16_t*)h, ldh, (const bf16_t*)dout, lddo,
+                                                                  (bf16_t*)dh, lddh, M, F);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_silu_fwd(const void* x, void* y, long long n, hipStream_t s) {
+  if (!x || !y || n % 8 || !al16(x) || !al16(y)) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  silu_fwd_kernel<<<grid_for(n / 8), 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n / 8);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_silu_bwd(const void* x, const void* dy, void* dx, long long n, hipStream_t s) {
+  if (!x || !dy || !dx || n % 8 || !al16(x) || !al16(dy) || !al16(dx)) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  silu_bwd_kernel<<<grid_for(n / 8), 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, n / 8);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_concat_channels(const void* a, long long lda, int Ca, const void* b, long long ldb, int Cb,
+                                    void* out, long long P, hipStream_t s) {
+  if (!a || !b || !out || Ca % 8 || Cb % 8 || lda % 8 || ldb % 8 || P < 0) return OTAMD_EINVAL;
+  if (!al16(a) || !al16(b) || !al16(out)) return OTAMD_EINVAL;
+  if (P == 0) return OTAMD_OK;
+  concat_kernel<<<grid_for(P * (Ca + Cb) / 8), 256, 0, s>>>((const bf16_t*)a, lda, Ca, (const bf16_t*)b, ldb, Cb,
+                                                            (bf16_t*)out, P);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_upsample2x_bwd(const void* dup, void* dx, int N, int H, int W, int C, int accumulate,
+                                   hipStream_t s) {
+  if (!dup || !dx || C % 8 || N <= 0 || H <= 0 || W <= 0 || !al16(dup) || !al16(dx)) return OTAMD_EINVAL;
+  upsample_bwd_kernel<<<grid_for((long long)N * H * W * C / 8), 256, 0, s>>>((const bf16_t*)dup, (bf16_t*)dx, N, H, W,
+                                                                             C, accumulate);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+// out: fp32 [groups][N], zeroed here
+OTAMD_API int otamd_colsum(const void* x, long long ldx, int M, int N, int rows_per_group, float* out, hipStream_t s) {
+  if (!x || !out || M <= 0 || N % 8 || ldx % 8 || rows_per_group <= 0 || !al16(x)) return OTAMD_EINVAL;
+  const int groups = (M + rows_per_group - 1) / rows_per_group;
+  if (hipMemsetAsync(out, 0, sizeof(float) * groups * (long long)N, s) != hipSuccess) return OTAMD_ELAUNCH;
+  const int cblocks = (N / 8 + 31) / 32;
+  const int rpb = 512;
+  const int rblocks = (rows_per_group + rpb - 1) / rpb;
+  dim3 grid(cblocks, rblocks, groups);
+  colsum_kernel<<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, M, N, rows_per_group, rpb, out);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_conv_weight_transpose(const void* w, void* wt, int Cout, int KK, int Cin, hipStream_t s) {
+  if (!w || !wt || Cout <= 0 || KK <= 0 || Cin <= 0) return OTAMD_EINVAL;
+  conv_wt_kernel<<<grid_for((long long)Cout * KK * Cin), 256, 0, s>>>((const bf16_t*)w, (bf16_t*)wt, Cout, KK, Cin);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t s) {
+  if (!x || !y || n < 0) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  cast_f2b_kernel<<<grid_for(n), 256, 0, s>>>(x, (bf16_t*)y, n);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_timestep_embedding(const float* t, int n, int dim, void* out, long long ldo, hipStream_t s) {
+  if (!t || !out || n <= 0 || dim % 2) return OTAMD_EINVAL;
+  timestep_embedding_kernel<<<grid_for((long long)n * dim / 2), 256, 0, s>>>(t, n, dim, (bf16_t*)out, ldo);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s) {
+  if (!a || !b || !y || n % 8 || !al16(a) || !al16(b) || !al16(y)) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  add_kernel<<<grid_for(n / 8), 256, 0, s>>>((const bf16_t*)a, (const bf16_t*)b, (bf16_t*)y, n / 8);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
