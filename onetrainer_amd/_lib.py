@@ -84,7 +84,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_upsample2x_bwd": [VP, VP, I, I, I, I, I, VP],
     "otamd_colsum": [VP, LL, I, I, I, VP, VP],
     "otamd_conv_weight_transpose": [VP, VP, I, I, I, VP],
-    "otamd_cast_f32_bf16": [VP, VP, LL, VP],
+    "otamd_cast_f32": [VP, VP, LL, I, I, VP],
     "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
     "otamd_add": [VP, VP, VP, LL, VP],
     # diffusion.hip

@@ -155,9 +155,17 @@ __global__ void conv_wt_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict_
   }
 }
 
-// fp32 -> bf16 cast (n elements) and bf16 -> fp32
-__global__ void cast_f2b_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
-  GRID_STRIDE(i, n) y[i] = f2bf(x[i]);
+// fp32 -> bf16 / f32 destination, optionally accumulating (grad writes of bias / norm params)
+__global__ void cast_f2b_kernel(const float* __restrict__ x, void* __restrict__ y, long long n, int dst_f32, int acc) {
+  GRID_STRIDE(i, n) {
+    if (dst_f32) {
+      float* d = reinterpret_cast<float*>(y);
+      d[i] = acc ? d[i] + x[i] : x[i];
+    } else {
+      bf16_t* d = reinterpret_cast<bf16_t*>(y);
+      d[i] = f2bf(acc ? bf2f(d[i]) + x[i] : x[i]);
+    }
+  }
 }
 
 // emb[b, :] = [cos(t*f_i), sin(t*f_i)], f_i = exp(-ln(10000) * i / half)   (flip_sin_to_cos=True, shift 0)
@@ -258,10 +266,10 @@ OTAMD_API int otamd_conv_weight_transpose(const void* w, void* wt, int Cout, int
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
-OTAMD_API int otamd_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t s) {
+OTAMD_API int otamd_cast_f32(const float* x, void* y, long long n, int dst_f32, int accumulate, hipStream_t s) {
   if (!x || !y || n < 0) return OTAMD_EINVAL;
   if (n == 0) return OTAMD_OK;
-  cast_f2b_kernel<<<grid_for(n), 256, 0, s>>>(x, (bf16_t*)y, n);
+  cast_f2b_kernel<<<grid_for(n), 256, 0, s>>>(x, y, n, dst_f32, accumulate);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

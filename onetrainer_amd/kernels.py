@@ -229,12 +229,11 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ksize=3, stride=1, pad=1, up
     N, P, Q, Cout, ldy = _nhwc(dy)
     N2, H, W, Cin, ldx = _nhwc(x)
     _req(N == N2 and conv_out_hw(H, W, ksize, stride, pad, upsample) == (P, Q), "wgrad geometry")
-    _req(ldy == Cout, "dy must be dense NHWC")
     if out is None:
         out = torch.empty((Cout, ksize, ksize, Cin), dtype=BF16, device=dy.device)
     _req(out.shape == (Cout, ksize, ksize, Cin) and out.is_contiguous(), "wgrad out")
     a = _new_args()
-    a.A, a.lda, a.amode = _p(dy), Cout, OPM_MN
+    a.A, a.lda, a.amode = _p(dy), ldy, OPM_MN
     a.B, a.ldb, a.bmode = _p(x), 8, OPM_CONV_WGRAD
     a.gb = _geom(N, H, W, Cin, P, Q, ksize, ksize, stride, pad, upsample, ldx)
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), ksize * ksize * Cin, int(out.dtype == F32), int(accumulate)
@@ -495,11 +494,13 @@ def conv_weight_transpose(w):
     return wt
 
 
-def cast_f32_bf16(x, out=None):
+def cast_f32_bf16(x, out=None, accumulate=False):
+    """fp32 -> out (bf16 or f32), optionally out += x."""
     _req(x.dtype == F32 and x.is_contiguous(), "f32 contiguous")
     out = torch.empty(x.shape, dtype=BF16, device=x.device) if out is None else out
-    _req(out.is_contiguous() and out.numel() == x.numel() and out.dtype == BF16, "bf16 out")
-    check(lib().otamd_cast_f32_bf16(_p(x), _p(out), x.numel(), stream_handle()), "otamd_cast_f32_bf16")
+    _req(out.is_contiguous() and out.numel() == x.numel() and out.dtype in (BF16, F32), "cast out")
+    check(lib().otamd_cast_f32(_p(x), _p(out), x.numel(), int(out.dtype == F32), int(accumulate), stream_handle()),
+          "otamd_cast_f32")
     return out
 
 

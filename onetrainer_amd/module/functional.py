@@ -1,0 +1,284 @@
+"""torch.autograd.Functions over the HIP kernels (onetrainer_amd/kernels.py).
+
+PyTorch hosts the tensors and the autograd graph; every forward/backward here launches the
+hand-written gfx950 kernels.  Parameter gradients never go through autograd: each Function
+receives a `PRef` (weight view + grad view in the FlatParamStore), writes the weight gradient
+in place (overwrite, or accumulate inside a gradient-accumulation window) and calls
+`store.mark_ready` so the DP reducer can launch that bucket's all-reduce while backward
+continues.  The nn.Parameters are still passed as inputs so autograd connects the graph; their
+returned gradient is None.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import kernels as K
+
+
+class PRef:
+    """A (possibly fused) trainable tensor: value view, grad view, member names, store."""
+    __slots__ = ("store", "names", "w", "g", "params")
+
+    def __init__(self, store, names, shape=None):
+        if isinstance(names, str):
+            names = [names]
+        self.store = store
+        self.names = list(names)
+        self.w = store.view(self.names, shape)
+        self.g = store.view(self.names, shape, grad=True)
+        self.params = tuple(store.params[n] for n in self.names)
+
+    def acc(self) -> bool:
+        return self.store.accumulate_into(self.names)
+
+    def done(self):
+        self.store.mark_ready(self.names)
+
+    def write_f32(self, src_f32: torch.Tensor):
+        """grad <- src (fp32 reduction result of a bias / norm-affine gradient)."""
+        K.cast_f32_bf16(src_f32.reshape(-1).contiguous(), out=self.g.view(-1), accumulate=self.acc())
+        self.done()
+
+
+def _params(*refs):
+    out = []
+    for r in refs:
+        if r is not None:
+            out.extend(r.params)
+    return out
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """2-D [rows, C] view of a token-major / NHWC tensor (keeps the row stride)."""
+    if t.dim() == 2:
+        return t
+    return t.reshape(-1, t.shape[-1]) if t.is_contiguous() else t.view(-1, t.shape[-1])
+
+
+# ----------------------------------------------------------------------------------------------
+class LinearFn(torch.autograd.Function):
+    """y = x @ W^T (+b) (+residual) over the last dim; x any [..., K] with unit inner stride."""
+
+    @staticmethod
+    def forward(ctx, x, wref, bref, residual, *params):
+        shp = x.shape
+        x2 = _rows(x)
+        r2 = _rows(residual) if residual is not None else None
+        y = K.linear(x2, wref.w, bias=bref.w if bref is not None else None, residual=r2)
+        ctx.save_for_backward(x2)
+        ctx.wref, ctx.bref, ctx.has_res, ctx.xshape = wref, bref, residual is not None, shp
+        return y.view(*shp[:-1], wref.w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x2,) = ctx.saved_tensors
+        wref, bref = ctx.wref, ctx.bref
+        dy2 = _rows(dy)
+        if dy2.stride(1) != 1 or dy2.stride(0) % 8:
+            dy2 = dy2.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.linear_dgrad(dy2, wref.w).view(ctx.xshape)
+        K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
+        wref.done()
+        if bref is not None:
+            bref.write_f32(K.colsum(dy2))
+        dres = dy if ctx.has_res else None
+        return (dx, None, None, dres) + (None,) * (len(ctx.needs_input_grad) - 4)
+
+
+def linear(x, wref, bref=None, residual=None):
+    return LinearFn.apply(x, wref, bref, residual, *_params(wref, bref))
+
+
+class ConvFn(torch.autograd.Function):
+    """NHWC conv 3x3 (pad 1), stride 1/2, optional virtual nearest-2x upsample of the input,
+    epilogue + bias + rowvec[n] (ResnetBlock2D time-embedding projection) + residual."""
+
+    @staticmethod
+    def forward(ctx, x, wref, bref, rowvec, residual, stride, upsample, *params):
+        y = K.conv2d(x, wref.w, bias=bref.w if bref is not None else None, stride=stride, pad=1, upsample=upsample,
+                     residual=residual, rowvec=rowvec)
+        ctx.save_for_backward(x)
+        ctx.wref, ctx.bref, ctx.stride, ctx.upsample = wref, bref, stride, upsample
+        ctx.has_rowvec, ctx.has_res = rowvec is not None, residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        wref, bref = ctx.wref, ctx.bref
+        if dy.stride(3) != 1 or dy.stride(2) % 8 or dy.stride(1) != dy.stride(2) * dy.shape[2] \
+                or dy.stride(0) != dy.stride(1) * dy.shape[1]:
+            dy = dy.contiguous()
+        N, H, W, _ = x.shape
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = K.conv_weight_transpose(wref.w)
+            if ctx.upsample:
+                dup = K.conv2d_dgrad(dy, wt, (2 * H, 2 * W), 1, 1)
+                dx = K.upsample2x_bwd(dup)
+            else:
+                dx = K.conv2d_dgrad(dy, wt, (H, W), ctx.stride, 1)
+        K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
+        wref.done()
+        drow = None
+        P, Q = dy.shape[1], dy.shape[2]
+        if ctx.has_rowvec:
+            per = K.colsum(dy, rows_per_group=P * Q)           # [N, Cout] fp32
+            drow = K.cast_f32_bf16(per.contiguous())
+            if bref is not None:
+                bref.write_f32(K.colsum(dy))
+        elif bref is not None:
+            bref.write_f32(K.colsum(dy))
+        dres = dy if ctx.has_res else None
+        return (dx, None, None, drow, dres, None, None) + (None,) * (len(ctx.needs_input_grad) - 7)
+
+
+def conv(x, wref, bref=None, rowvec=None, residual=None, stride=1, upsample=False):
+    return ConvFn.apply(x, wref, bref, rowvec, residual, stride, upsample, *_params(wref, bref))
+
+
+class GroupNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gref, bref, groups, eps, silu, *params):
+        y, stats = K.groupnorm_fwd(x, gref.w, bref.w, groups, eps, silu)
+        ctx.save_for_backward(x, *stats)
+        ctx.gref, ctx.bref, ctx.groups, ctx.silu = gref, bref, groups, silu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, *stats = ctx.saved_tensors
+        dx, dg, db = K.groupnorm_bwd(x, dy, ctx.gref.w, ctx.groups, ctx.silu, stats)
+        ctx.gref.write_f32(dg)
+        ctx.bref.write_f32(db)
+        return (dx if ctx.needs_input_grad[0] else None,) + (None,) * (len(ctx.needs_input_grad) - 1)
+
+
+def group_norm(x, gref, bref, groups, eps, silu):
+    return GroupNormFn.apply(x, gref, bref, groups, eps, silu, *_params(gref, bref))
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gref, bref, eps, *params):
+        y, stats = K.layernorm_fwd(x, gref.w, bref.w, eps)
+        ctx.save_for_backward(x, *stats)
+        ctx.gref, ctx.bref = gref, bref
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, *stats = ctx.saved_tensors
+        if dy.stride(-1) != 1:
+            dy = dy.contiguous()
+        dx, dg, db = K.layernorm_bwd(x, dy, ctx.gref.w, stats)
+        ctx.gref.write_f32(dg)
+        ctx.bref.write_f32(db)
+        return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
+
+
+def layer_norm(x, gref, bref, eps=1e-5):
+    return LayerNormFn.apply(x, gref, bref, eps, *_params(gref, bref))
+
+
+class SelfAttnFn(torch.autograd.Function):
+    """qkv [B, N, 3C] (fused projection output) -> o [B, N, C]."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        C = qkv.shape[-1] // 3
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        o, lse = K.attn_fwd(q, k, v, heads)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.heads = heads
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        C = qkv.shape[-1] // 3
+        dqkv = torch.empty_like(qkv)
+        K.attn_bwd(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], o, lse, do, ctx.heads,
+                   dq=dqkv[..., :C], dk=dqkv[..., C:2 * C], dv=dqkv[..., 2 * C:])
+        return dqkv, None
+
+
+class CrossAttnFn(torch.autograd.Function):
+    """q [B, N, C], kv [B, L, 2C] -> o [B, N, C]."""
+
+    @staticmethod
+    def forward(ctx, q, kv, heads):
+        C = q.shape[-1]
+        o, lse = K.attn_fwd(q, kv[..., :C], kv[..., C:], heads)
+        ctx.save_for_backward(q, kv, o, lse)
+        ctx.heads = heads
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, kv, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        C = q.shape[-1]
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:])
+        return dq, (dkv if ctx.needs_input_grad[1] else None), None
+
+
+class GEGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h):
+        ctx.save_for_backward(h)
+        return K.geglu_fwd(h)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (h,) = ctx.saved_tensors
+        return K.geglu_bwd(h, dy.contiguous())
+
+
+class SiLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return K.silu_fwd(x.contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return K.silu_bwd(x.contiguous(), dy.contiguous())
+
+
+class ConcatFn(torch.autograd.Function):
+    """channel concat of two NHWC tensors (UNet up-block skip connection)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.ca = a.shape[-1]
+        return K.concat_channels(a, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy[..., :ctx.ca], dy[..., ctx.ca:]
+
+
+class MSELossFn(torch.autograd.Function):
+    """ModelSetupDiffusionLossMixin.__unmasked_losses + _diffusion_losses + .mean() (+ /GA)."""
+
+    @staticmethod
+    def forward(ctx, pred, target, loss_weight, timestep, coeffs, loss_fn, gamma, v_pred, ga, mse_strength, scale):
+        loss, coef, losses = K.mse_loss(pred, target, loss_weight, mse_strength=mse_strength, scale=scale,
+                                        loss_fn=loss_fn, gamma=gamma, v_pred=v_pred, ga=ga, timestep=timestep,
+                                        coeffs=coeffs)
+        ctx.save_for_backward(pred, target, coef)
+        ctx.losses = losses
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, target, coef = ctx.saved_tensors
+        gd = g.reshape(1).float().contiguous()
+        return (K.mse_grad(pred, target, coef, grad_out=gd),) + (None,) * 10

@@ -1,0 +1,115 @@
+"""Flat parameter / gradient store.
+
+All trainable tensors of a model live as views of ONE flat buffer (params) with a twin flat
+buffer for gradients, each tensor at a 16-byte aligned offset.  Consequences:
+  * the fused AdamW (csrc/adamw.hip) is a single pass over the flat buffers (14 B/param bf16);
+  * data-parallel gradient buckets are contiguous slices of the flat grad buffer (trainer/ddp.py);
+  * weights that one GEMM consumes together (to_q|to_k|to_v, to_k|to_v) are adjacent, so the
+    fused projection weight and its gradient are plain views -- no concat, no split.
+Backward kernels write weight gradients straight into `grad` views (overwrite on the first
+micro-step of an accumulation window, accumulate afterwards) and call `mark_ready`, which feeds
+the DP reducer; autograd never materialises or accumulates parameter gradients.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+
+@dataclass
+class Slot:
+    name: str
+    shape: tuple
+    offset: int
+    numel: int
+    group: str
+
+
+class FlatParamStore:
+    def __init__(self, specs, dtype, device, align_bytes=16):
+        """specs: iterable of (name, shape, group) in layout order."""
+        esz = torch.tensor([], dtype=dtype).element_size()
+        al = max(1, align_bytes // esz)
+        self.dtype, self.device = dtype, device
+        self.slots: dict[str, Slot] = {}
+        self.order: list[str] = []
+        off = 0
+        for name, shape, group in specs:
+            n = 1
+            for s in shape:
+                n *= int(s)
+            off = (off + al - 1) // al * al
+            self.slots[name] = Slot(name, tuple(int(s) for s in shape), off, n, group)
+            self.order.append(name)
+            off += n
+        self.numel = (off + al - 1) // al * al
+        self.data = torch.zeros(self.numel, dtype=dtype, device=device)
+        self.grad = torch.zeros(self.numel, dtype=dtype, device=device)
+        self.params: dict[str, torch.nn.Parameter] = {}
+        for name in self.order:
+            s = self.slots[name]
+            p = torch.nn.Parameter(self.data[s.offset:s.offset + s.numel].view(s.shape))
+            p.grad = self.grad[s.offset:s.offset + s.numel].view(s.shape)
+            self.params[name] = p
+        self._written: set[str] = set()
+        self.accumulating = False          # True on micro-steps after the first of a GA window
+        self.ready_hooks = []              # callables(names) -> None (DP reducer)
+
+    # ----- views -------------------------------------------------------------------------------
+    def view(self, names, shape=None, grad=False):
+        """contiguous view spanning `names` (which must be adjacent without padding)."""
+        if isinstance(names, str):
+            names = [names]
+        first = self.slots[names[0]]
+        end = first.offset
+        for n in names:
+            s = self.slots[n]
+            if s.offset != end:
+                raise ValueError(f"parameters {names} are not adjacent in the flat store")
+            end += s.numel
+        buf = self.grad if grad else self.data
+        v = buf[first.offset:end]
+        if shape is not None:
+            v = v.view(shape)
+        elif len(names) == 1:
+            v = v.view(first.shape)
+        return v
+
+    def range_of(self, names):
+        first = self.slots[names[0]]
+        last = self.slots[names[-1]]
+        return first.offset, last.offset + last.numel
+
+    # ----- gradient bookkeeping -----------------------------------------------------------------
+    def accumulate_into(self, names) -> bool:
+        """True if a backward kernel must add into the grad view (GA window), else overwrite."""
+        return self.accumulating
+
+    def mark_ready(self, names):
+        self._written.update(names)
+        for h in self.ready_hooks:
+            h(names)
+
+    def begin_backward(self):
+        self._written.clear()
+
+    def finish_backward(self):
+        """zero the grads of parameters that received none this micro-step (overwrite semantics)."""
+        if not self.accumulating:
+            for n in self.order:
+                if n not in self._written:
+                    s = self.slots[n]
+                    self.grad[s.offset:s.offset + s.numel].zero_()
+
+    def named_parameters(self):
+        return [(n, self.params[n]) for n in self.order]
+
+    def group_ranges(self):
+        """{group: (begin, end)} element ranges; groups must be contiguous in layout order."""
+        out = {}
+        for n in self.order:
+            s = self.slots[n]
+            b, e = out.get(s.group, (s.offset, s.offset + s.numel))
+            out[s.group] = (min(b, s.offset), max(e, s.offset + s.numel))
+        return out
