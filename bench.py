@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Benchmark: SDXL 1.0 UNet full fine-tune train step, 1024^2 (128^2 latents), bf16, b=4 per GPU.
+
+BASELINE.json metric "train images/sec (whole node) + step-time p50, SDXL 1024^2 bf16 at 1/2/4/8 GPU";
+workload = configs[2] (SDXL full-finetune 1024^2, global batch 32 = 8 x 4) run per GPU at b=4
+(weak scaling: per-GPU work fixed).  A step is the reference's GenericTrainer step body
+(GenericTrainer.py:672-749): predict (noise, timesteps, DDPM noising, UNet fwd) -> MSE loss ->
+backward -> [DP all-reduce] -> clip_grad_norm(1.0) -> AdamW(+bf16 SR) -> LR step.  Inputs are
+synthetic cached latents/text states resident in HBM; weights random (no network here).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (driver, N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(res=512, steps=1):
+    """Oracle (CPU fp32 restatement of the reference step: diffusers UNet + DDPM noise + MSE +
+    clip + torch AdamW) timed on this host's cores, SDXL at `res`^2, batch 1."""
+    from oracle import unet as OU
+    from oracle import diffusion as OD
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    cfg = OU.sdxl_config()
+    torch.manual_seed(0)
+    t0 = time.time()
+    with torch.device("meta"):
+        m = OU.UNet2DConditionModel(cfg)
+    m = m.to_empty(device="cpu")
+    with torch.no_grad():
+        for p in m.parameters():
+            p.uniform_(-0.02, 0.02)
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-6, weight_decay=1e-2, foreach=True)
+    betas = OD.scaled_linear_betas()
+    h = res // 8
+    x0 = torch.randn(1, 4, h, h)
+    ehs = torch.randn(1, 77, 2048)
+    te = torch.randn(1, 1280)
+    tid = torch.tensor([[float(res), float(res), 0., 0., float(res), float(res)]])
+    build_s = time.time() - t0
+
+    def step(i):
+        g = torch.Generator().manual_seed(i)
+        eps = OD.create_noise(x0.shape, g)
+        t = OD.timestep_discrete(1000, 1, g)
+        xt = OD.add_noise_ddpm(x0, eps, t, betas)
+        pred = m(xt, t, ehs, te, tid)
+        loss = OD.diffusion_losses(pred, eps, torch.ones(1)).mean()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    t0 = time.time()
+    for i in range(steps):
+        step(i)
+    dt = (time.time() - t0) / steps
+    del m, opt
+    return dt, threads, build_s
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4, help="per-GPU batch")
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-res", type=int, default=512)
+    args = ap.parse_args()
+
+    from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_sdxl_batch
+    from onetrainer_amd.module.unet import flops_per_image, sdxl_config
+    from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+
+    cfg = TrainConfig.default_values()
+    cfg.batch_size = args.batch
+    cfg.learning_rate = 3e-6
+    cfg.learning_rate_warmup_steps = 0
+    cfg.resolution = str(args.res)
+
+    tr = GenericTrainer(cfg)
+    t0 = time.time()
+    tr.start()
+    rank, world = tr.rank, tr.world
+    dev = tr.device
+    log(f"[bench] rank {rank}/{world} model ready in {time.time() - t0:.1f}s "
+        f"({tr.model.unet.num_parameters() / 1e9:.3f} B params)")
+    batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=rank)
+
+    for i in range(args.warmup):
+        tr.train_step(batch)
+        if i == 0:
+            torch.cuda.synchronize()
+            log(f"[bench] first step done, mem {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t_start = time.perf_counter()
+    evs[0].record(stream)
+    losses = []
+    for i in range(args.steps):
+        losses.append(tr.train_step(batch))
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    p50 = step_ms[len(step_ms) // 2]
+    p90 = step_ms[min(len(step_ms) - 1, int(0.9 * len(step_ms)))]
+    loss_last = torch.stack(losses).float().mean()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        dist.all_reduce(loss_last)
+        loss_last /= world
+    loss_val = loss_last.item()
+    if not math.isfinite(loss_val):
+        raise RuntimeError(f"non-finite loss {loss_val}")
+
+    imgs = args.batch * world * args.steps
+    value = imgs / elapsed
+    ms = 1000.0 * elapsed / args.steps
+    fwd_tf = flops_per_image(sdxl_config(), args.res // 8, args.res // 8) / 1e12
+    train_tf_img = 3.0 * fwd_tf                       # fwd + dgrad + wgrad
+    achieved = train_tf_img * args.batch / (ms / 1000.0)   # per GPU, TFLOP/s
+    out = {
+        "metric": "train images/sec (whole node) + step-time p50, SDXL 1024^2 bf16",
+        "value": round(value, 3),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 2),
+        "step_ms_p50": round(p50, 2),
+        "step_ms_p90": round(p90, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (random cached latents/text states, random-init weights)",
+        "config": {"workload": f"SDXL 1.0 UNet full fine-tune train step {args.res}^2 (latent {args.res // 8}^2), "
+                               f"b={args.batch}/GPU, AdamW+bf16 SR, clip 1.0",
+                   "model": "SDXL 1.0 UNet (2.567B params)", "global_batch": args.batch * world,
+                   "seq_len": (args.res // 8) ** 2, "parallelism": f"dp{world}"},
+        "loss": round(loss_val, 5),
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "basis": f"{train_tf_img:.3f} TFLOP/image algorithmic (3 x {fwd_tf:.3f} fwd) x per-GPU images / "
+                              "step time"},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del tr
+        torch.cuda.empty_cache()
+        log("[bench] cpu baseline (oracle, fp32) ...")
+        try:
+            dt, threads, build_s = cpu_baseline(args.cpu_res, 1)
+            cpu_tf = 3.0 * flops_per_image(sdxl_config(), args.cpu_res // 8, args.cpu_res // 8) / 1e12
+            eq = (1.0 / dt) * cpu_tf / train_tf_img        # images/s at the bench resolution, by FLOP ratio
+            out["cpu_baseline"] = {"value": round(eq, 5), "unit": "images/s", "cores": threads, "kind": "port",
+                                   "sample": f"1 step of the oracle (CPU fp32 restatement: UNet fwd+bwd, DDPM noise, "
+                                             f"MSE, clip, torch AdamW) at SDXL {args.cpu_res}^2 b=1 took {dt:.2f}s; "
+                                             f"value scaled to {args.res}^2 by the FLOP ratio "
+                                             f"({cpu_tf:.2f}/{train_tf_img:.2f} TFLOP)"}
+        except Exception as e:   # the baseline must not sink the GPU measurement
+            out["cpu_baseline"] = {"value": None, "unit": "images/s", "cores": None, "kind": "port",
+                                   "sample": f"failed: {e!r}"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,101 @@
+"""predict / calculate_loss for SDXL (and SD1.5: no add-embedding) on the HIP kernels.
+
+Drop-in for modules/modelSetup/BaseStableDiffusionXLSetup.py:179-373 (predict, calculate_loss),
+with the math of ModelSetupNoiseMixin.py:18-155, ModelSetupDiffusionMixin.py:15-38 and
+ModelSetupDiffusionLossMixin.py:119-279 done by csrc/diffusion.hip:
+  * noise / timesteps: Philox, seeded by the same `batch_seed` (0 if deterministic else
+    global_step); counter = index in the GLOBAL batch, so DP rank r draws exactly its slice;
+  * DDPM noising + target (epsilon / v_prediction) in one prologue kernel;
+  * unmasked MSE (+ MIN_SNR_GAMMA / DEBIASED_ESTIMATION / P2 weights, loss_weight, scalers).
+Batch contract as the reference's data loader (StableDiffusionXLBaseDataLoader.py:174-209),
+except that `latent_image` may be NHWC [B,h,w,4] (this build's loader) or NCHW [B,4,h,w].
+"""
+from __future__ import annotations
+
+from random import Random
+
+import torch
+
+from .. import kernels as K
+from ..module import functional as Fn
+
+LOSS_FN = {"CONSTANT": 0, "MIN_SNR_GAMMA": 1, "DEBIASED_ESTIMATION": 2, "P2": 3}
+
+
+class BaseStableDiffusionXLSetup:
+    def __init__(self, train_device, temp_device=None, debug_mode=False, dp_rank=0, dp_world=1):
+        self.train_device = torch.device(train_device)
+        self.temp_device = temp_device
+        self.debug_mode = debug_mode
+        self.dp_rank = dp_rank
+        self.dp_world = dp_world
+
+    # ------------------------------------------------------------------------------------------
+    @staticmethod
+    def _nhwc_latent(lat: torch.Tensor) -> torch.Tensor:
+        if lat.dim() == 4 and lat.shape[1] == 4 and lat.shape[-1] != 4:
+            lat = lat.permute(0, 2, 3, 1)
+        return lat.contiguous()
+
+    def _text(self, model, batch, config, rand, B):
+        te1 = batch["text_encoder_1_hidden_state"]
+        te2 = batch.get("text_encoder_2_hidden_state")
+        pooled = batch.get("text_encoder_2_pooled_state")
+        for part, key in ((config.text_encoder, "te1"), (config.text_encoder_2, "te2")):
+            p = part.dropout_probability
+            if p is not None and p > 0:   # StableDiffusionXLModel.py:266-281 (host mask from Random(seed))
+                mask = torch.tensor([rand.random() > p for _ in range(B)], device=te1.device).to(te1.dtype)
+                if key == "te1":
+                    te1 = te1 * mask[:, None, None]
+                else:
+                    te2 = te2 * mask[:, None, None]
+                    pooled = pooled * mask[:, None]
+        ehs, pooled = model.combine_text_encoder_output(te1.to(torch.bfloat16), None if te2 is None else
+                                                        te2.to(torch.bfloat16), pooled)
+        return ehs, pooled
+
+    def predict(self, model, batch: dict, config, train_progress, *, deterministic: bool = False) -> dict:
+        if config.offset_noise_weight > 0 or config.perturbation_noise_weight > 0:
+            raise NotImplementedError("offset / perturbation noise are not on this build's hot path yet")
+        batch_seed = 0 if deterministic else train_progress.global_step
+        rand = Random(batch_seed)
+        latent = self._nhwc_latent(batch["latent_image"])
+        B, h, w, C = latent.shape
+        sf = model.vae.config["scaling_factor"]
+        ehs, pooled = self._text(model, batch, config, rand, B)
+        sample0 = self.dp_rank * B                       # global-batch index of this rank's first sample
+        noise = K.noise(latent.shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=latent.dtype,
+                        device=latent.device)
+        N = model.noise_scheduler.config["num_train_timesteps"]
+        if deterministic:
+            timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=latent.device)
+        else:
+            dist = {"UNIFORM": 0, "LOGIT_NORMAL": 1}[config.timestep_distribution]
+            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=dist, num_train_timesteps=N,
+                                   min_s=config.min_noising_strength, max_s=config.max_noising_strength,
+                                   shift=config.timestep_shift, bias=config.noising_bias,
+                                   weight=config.noising_weight, device=latent.device)
+        ptype = model.noise_scheduler.config["prediction_type"]
+        unet_in, target, _ = K.ddpm_prologue(latent, noise, timestep, model.noise_scheduler.coeffs, sf,
+                                             1 if ptype == "v_prediction" else 0)
+        time_ids = None
+        if model.unet.cfg.addition_embed:
+            time_ids = torch.stack([batch["original_resolution"][0], batch["original_resolution"][1],
+                                    batch["crop_offset"][0], batch["crop_offset"][1],
+                                    batch["crop_resolution"][0], batch["crop_resolution"][1]], dim=1).to(
+                latent.device, torch.float32)
+        pred = model.unet(unet_in, timestep, ehs, pooled, time_ids)
+        return {"loss_type": "target", "timestep": timestep, "predicted": pred, "target": target,
+                "prediction_type": ptype}
+
+    def calculate_loss(self, model, batch: dict, data: dict, config) -> torch.Tensor:
+        if config.mae_strength != 0 or config.log_cosh_strength != 0 or config.masked_training:
+            raise NotImplementedError("only the unmasked MSE loss of C1-C5 is on this build's hot path")
+        bs = 1 if config.loss_scaler in ("NONE", "GRADIENT_ACCUMULATION") else config.batch_size
+        gas = 1 if config.loss_scaler in ("NONE", "BATCH") else config.gradient_accumulation_steps
+        lw = batch.get("loss_weight")
+        lw = lw.to(self.train_device, torch.float32).contiguous() if lw is not None else None
+        return Fn.MSELossFn.apply(data["predicted"], data["target"], lw, data["timestep"],
+                                  model.noise_scheduler.coeffs, LOSS_FN[config.loss_weight_fn],
+                                  config.loss_weight_strength, data.get("prediction_type") == "v_prediction", 1.0,
+                                  config.mse_strength, float(bs * gas), 1.0 / self.dp_world)

@@ -30,7 +30,7 @@ class FlatParamStore:
     def __init__(self, specs, dtype, device, align_bytes=16):
         """specs: iterable of (name, shape, group) in layout order."""
         esz = torch.tensor([], dtype=dtype).element_size()
-        al = max(1, align_bytes // esz)
+        al = max(8, align_bytes // esz)   # >= 8 elements: the grad-norm kernel reads 8-wide chunks
         self.dtype, self.device = dtype, device
         self.slots: dict[str, Slot] = {}
         self.order: list[str] = []

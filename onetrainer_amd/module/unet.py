@@ -200,13 +200,13 @@ class UNet2DConditionModel:
     # ----- parameters ---------------------------------------------------------------------------
     def init_weights(self, seed: int):
         """torch default init of diffusers modules: U(-1/sqrt(fan_in), 1/sqrt(fan_in)); norms 1/0."""
-        g = torch.Generator(device="cpu").manual_seed(seed)
+        g = torch.Generator(device=self.device).manual_seed(seed)
         with torch.no_grad():
             for name, shape, kind, fan_in in self.specs:
                 p = self.store.params[name]
                 if kind in ("linear", "conv", "bias"):
                     bound = 1.0 / math.sqrt(fan_in)
-                    val = (torch.rand(shape, generator=g) * 2 - 1) * bound
+                    val = (torch.rand(shape, generator=g, device=self.device) * 2 - 1) * bound
                     self._assign(name, val, kind)
                 elif kind == "norm_w":
                     p.fill_(1.0)

@@ -1,0 +1,118 @@
+"""TrainConfig subset consumed by the hot path, loadable from the reference's own JSON.
+
+Mirrors modules/util/config/TrainConfig.py (defaults at 759-995, optimizer part 114-195) for
+exactly the fields the train step reads; unknown keys of a reference config /
+training preset are kept in `extra` and ignored, so `training_presets/#sdxl 1.0.json` and a
+reference `config.json` load unchanged.  New build-only knobs (data-parallel, bench) live in
+their own fields with defaults that keep the reference behaviour.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field, fields
+
+
+@dataclass
+class OptimizerConfig:
+    optimizer: str = "ADAMW"
+    beta1: float | None = None
+    beta2: float | None = None
+    eps: float | None = None
+    weight_decay: float | None = None
+    stochastic_rounding: bool = True
+    fused_back_pass: bool = False
+    foreach: bool | None = False
+    fused: bool | None = False
+
+
+@dataclass
+class ModelPartConfig:
+    train: bool = True
+    learning_rate: float | None = None
+    weight_dtype: str = "NONE"
+    dropout_probability: float = 0.0
+
+
+@dataclass
+class TrainConfig:
+    model_type: str = "STABLE_DIFFUSION_XL_10_BASE"
+    training_method: str = "FINE_TUNE"
+    train_device: str = "cuda"
+    temp_device: str = "cpu"
+    train_dtype: str = "BFLOAT_16"
+    weight_dtype: str = "BFLOAT_16"
+    resolution: str = "1024"
+    batch_size: int = 1
+    gradient_accumulation_steps: int = 1
+    epochs: int = 100
+    learning_rate: float = 3e-6
+    learning_rate_scheduler: str = "CONSTANT"
+    learning_rate_warmup_steps: float = 200.0
+    learning_rate_cycles: float = 1.0
+    learning_rate_min_factor: float = 0.0
+    clip_grad_norm: float | None = 1.0
+    # noise / timesteps (ModelSetupNoiseMixin)
+    offset_noise_weight: float = 0.0
+    perturbation_noise_weight: float = 0.0
+    timestep_distribution: str = "UNIFORM"
+    min_noising_strength: float = 0.0
+    max_noising_strength: float = 1.0
+    noising_weight: float = 0.0
+    noising_bias: float = 0.0
+    timestep_shift: float = 1.0
+    dynamic_timestep_shifting: bool = False
+    # loss (ModelSetupDiffusionLossMixin)
+    mse_strength: float = 1.0
+    mae_strength: float = 0.0
+    log_cosh_strength: float = 0.0
+    vb_loss_strength: float = 1.0
+    loss_weight_fn: str = "CONSTANT"
+    loss_weight_strength: float = 5.0
+    loss_scaler: str = "NONE"
+    masked_training: bool = False
+    # LoRA
+    lora_rank: int = 16
+    lora_alpha: float = 1.0
+    lora_weight_dtype: str = "FLOAT_32"
+    lora_layers: str = ""
+    # parts
+    optimizer: OptimizerConfig = field(default_factory=OptimizerConfig)
+    unet: ModelPartConfig = field(default_factory=ModelPartConfig)
+    text_encoder: ModelPartConfig = field(default_factory=lambda: ModelPartConfig(train=False))
+    text_encoder_2: ModelPartConfig = field(default_factory=lambda: ModelPartConfig(train=False))
+    vae: ModelPartConfig = field(default_factory=lambda: ModelPartConfig(train=False))
+    prior: ModelPartConfig = field(default_factory=ModelPartConfig)
+    # build-only (not in the reference): data parallel + gradient bucket size
+    dp_bucket_mb: int = 256
+    extra: dict = field(default_factory=dict)
+
+    @staticmethod
+    def default_values() -> "TrainConfig":
+        return TrainConfig()
+
+    def from_dict(self, d: dict) -> "TrainConfig":
+        names = {f.name: f for f in fields(self)}
+        for k, v in d.items():
+            if k in names and k != "extra":
+                cur = getattr(self, k)
+                if isinstance(cur, (OptimizerConfig, ModelPartConfig)) and isinstance(v, dict):
+                    for kk, vv in v.items():
+                        if hasattr(cur, kk):
+                            setattr(cur, kk, vv)
+                else:
+                    setattr(self, k, v)
+            else:
+                self.extra[k] = v
+        return self
+
+    @staticmethod
+    def load(path: str) -> "TrainConfig":
+        with open(path) as f:
+            return TrainConfig().from_dict(json.load(f))
+
+    def resolution_hw(self) -> tuple[int, int]:
+        r = str(self.resolution)
+        if "x" in r:
+            h, w = r.split("x")
+            return int(h), int(w)
+        return int(r), int(r)

@@ -1,0 +1,34 @@
+"""Factories (mirrors the parts of modules/util/create.py the hot path uses:
+create_model_setup 285-353, create_optimizer 509-534 via setup_model, create_lr_scheduler
+1114-1232, create_noise_scheduler 1235-1373)."""
+from __future__ import annotations
+
+import torch
+
+from ..model.StableDiffusionXLModel import NoiseScheduler, StableDiffusionXLModel
+from ..module import unet as U
+from ..util.lr_scheduler_util import create_lr_scheduler  # noqa: F401  (re-export)
+
+SCALING = {"STABLE_DIFFUSION_XL_10_BASE": 0.13025, "STABLE_DIFFUSION_15": 0.18215}
+
+
+def create_model(config, device, seed=0, unet_config=None, prediction_type="epsilon"):
+    """random-weight model of the configured architecture (weights from disk: SURVEY.md §8(f) #2)."""
+    mt = config.model_type
+    if unet_config is None:
+        if mt.startswith("STABLE_DIFFUSION_XL"):
+            unet_config = U.sdxl_config()
+        elif mt.startswith("STABLE_DIFFUSION_15") or mt == "STABLE_DIFFUSION_15":
+            unet_config = U.sd15_config()
+        else:
+            raise NotImplementedError(f"model type {mt}")
+    unet = U.UNet2DConditionModel(unet_config, device, seed=seed)
+    ns = NoiseScheduler(device, prediction_type=prediction_type)
+    return StableDiffusionXLModel(unet, ns, SCALING.get(mt, 0.13025), model_type=mt)
+
+
+def create_model_setup(config, train_device, dp_rank=0, dp_world=1):
+    if config.training_method == "FINE_TUNE":
+        from ..modelSetup.StableDiffusionXLFineTuneSetup import StableDiffusionXLFineTuneSetup
+        return StableDiffusionXLFineTuneSetup(train_device, dp_rank=dp_rank, dp_world=dp_world)
+    raise NotImplementedError(f"training method {config.training_method}")

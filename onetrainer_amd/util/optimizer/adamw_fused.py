@@ -1,0 +1,169 @@
+"""Fused multi-tensor AdamW (+ bf16 stochastic rounding) over a FlatParamStore.
+
+Drop-in for what the reference builds at modules/util/create.py:509-534:
+    torch.optim.AdamW(params, lr, betas, weight_decay, eps, foreach=False, fused=False)
+    patch_adamw(optimizer, stochastic_rounding)          # modules/util/optimizer/adamw_extensions.py:202-205
+plus the global clip the trainer applies before step() (modules/trainer/GenericTrainer.py:712-713).
+Same optimizer contract: param_groups with 'lr' (LambdaLR drives it), step(),
+zero_grad(set_to_none), state_dict()/load_state_dict() (torch AdamW layout: per-param 'step',
+'exp_avg', 'exp_avg_sq'), step_parameter(p, group, i).  The arithmetic is one launch over the
+flat store (csrc/adamw.hip) instead of ~8 torch ops per tensor.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+from ... import _lib
+from ... import kernels as K
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, store, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 stochastic_rounding=True, seed=0):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
+                        foreach=False, capturable=False, differentiable=False, fused=False)
+        super().__init__(param_groups, defaults)
+        self.store = store
+        self.stochastic_rounding = stochastic_rounding
+        self.seed = seed
+        self.exp_avg = torch.zeros_like(store.data)
+        self.exp_avg_sq = torch.zeros_like(store.data)
+        self._ptr2name = {store.params[n].data_ptr(): n for n in store.order}
+        self._ranges = []
+        for g in self.param_groups:
+            offs = []
+            for p in g["params"]:
+                s = store.slots[self._ptr2name[p.data_ptr()]]
+                offs.append((s.offset, s.offset + s.numel))
+            b, e = min(o[0] for o in offs), max(o[1] for o in offs)
+            covered = sum(o[1] - o[0] for o in offs)
+            span = [s for s in store.order if b <= store.slots[s].offset < e]
+            if len(span) != len(offs):
+                raise ValueError("each optimizer param group must be a contiguous range of the flat store")
+            self._ranges.append((b, e))
+            del covered
+        self.steps = [0 for _ in self.param_groups]
+        # per-tensor chunk table for the global grad norm
+        chunks = []
+        for ti, n in enumerate(store.order):
+            s = store.slots[n]
+            for c0 in range(s.offset, s.offset + s.numel, 1 << 16):
+                chunks.append((c0, min(s.offset + s.numel, c0 + (1 << 16)), ti))
+        arr = (_lib.NormChunk * len(chunks))()
+        for i, (b, e, t) in enumerate(chunks):
+            arr[i].begin, arr[i].end, arr[i].tensor = b, e, t
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self._chunks = raw.to(store.device)
+        self._n_chunks = len(chunks)
+        self._tensor_sq = torch.zeros(len(store.order), dtype=torch.float64, device=store.device)
+        self.clip_out = torch.zeros(2, dtype=torch.float32, device=store.device)   # [coef, total norm]
+
+    # --- clip_grad_norm_ (GenericTrainer.py:712-713) ----------------------------------------------
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """computes the clip coefficient on device; it is applied inside the next step()."""
+        K.grad_clip_coef(self.store.grad, self._chunks, self._n_chunks, self._tensor_sq, len(self.store.order),
+                         max_norm, self.clip_out)
+        self._pending_clip = True
+        return self.clip_out[1]
+
+    def _groups_struct(self, idx_list, steps=None):
+        arr = []
+        for k, gi in enumerate(idx_list):
+            g = self.param_groups[gi]
+            if steps is None:
+                self.steps[gi] += 1
+                step = self.steps[gi]
+            else:
+                step = steps[k]
+            lr = float(g["lr"])
+            beta1, beta2 = g["betas"]
+            bc1 = 1 - beta1 ** step
+            bc2 = 1 - beta2 ** step
+            s = _lib.AdamwGroup()
+            s.begin, s.end = self._ranges[gi]
+            s.wd_factor = 1 - lr * g["weight_decay"]
+            s.one_minus_beta1 = 1 - beta1
+            s.beta2 = beta2
+            s.one_minus_beta2 = 1 - beta2
+            s.bc2_sqrt = math.sqrt(bc2)
+            s.eps = g["eps"]
+            s.neg_step_size = -(lr / bc1)
+            arr.append(s)
+        order = sorted(range(len(arr)), key=lambda i: arr[i].begin)
+        return [arr[i] for i in order]
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        groups = self._groups_struct(range(len(self.param_groups)))
+        clip = self.clip_out if getattr(self, "_pending_clip", False) else None
+        self._pending_clip = False
+        st = self.store
+        if st.dtype == torch.bfloat16:
+            self.seed = (self.seed * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
+            K.adamw_bf16(st.data, st.grad, self.exp_avg, self.exp_avg_sq, groups, clip_coef=clip,
+                         stochastic_rounding=self.stochastic_rounding, seed=self.seed)
+        else:
+            K.adamw_f32(st.data, st.grad, self.exp_avg, self.exp_avg_sq, groups, clip_coef=clip)
+        return loss
+
+    def step_parameter(self, p, group, i):
+        """fused-back-pass API (adamw_extensions.py:202-205): update one parameter tensor."""
+        gi = self.param_groups.index(group)
+        name = self._ptr2name[p.data_ptr()]
+        s = self.store.slots[name]
+        if not hasattr(self, "_pstep"):
+            self._pstep = {}
+        self._pstep[name] = self._pstep.get(name, self.steps[gi]) + 1
+        saved = self._ranges[gi]
+        self._ranges[gi] = (s.offset, s.offset + s.numel)
+        try:
+            groups = self._groups_struct([gi], steps=[self._pstep[name]])
+        finally:
+            self._ranges[gi] = saved
+        st = self.store
+        K.adamw_bf16(st.data, st.grad, self.exp_avg, self.exp_avg_sq, groups, clip_coef=None,
+                     stochastic_rounding=self.stochastic_rounding, seed=self.seed)
+
+    def zero_grad(self, set_to_none: bool = True):
+        """grads are views of the flat store that the next backward overwrites; nothing to clear."""
+        self.store.accumulating = False
+
+    # --- torch AdamW-compatible state -------------------------------------------------------------
+    def state_dict(self):
+        state = {}
+        idx = 0
+        groups = []
+        for gi, g in enumerate(self.param_groups):
+            ids = []
+            for p in g["params"]:
+                s = self.store.slots[self._ptr2name[p.data_ptr()]]
+                sl = slice(s.offset, s.offset + s.numel)
+                state[idx] = {"step": torch.tensor(float(self.steps[gi])),
+                              "exp_avg": self.exp_avg[sl].view(s.shape).clone(),
+                              "exp_avg_sq": self.exp_avg_sq[sl].view(s.shape).clone()}
+                ids.append(idx)
+                idx += 1
+            gd = {k: v for k, v in g.items() if k != "params"}
+            gd["params"] = ids
+            groups.append(gd)
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        idx = 0
+        for gi, (g, gsd) in enumerate(zip(self.param_groups, sd["param_groups"])):
+            for k, v in gsd.items():
+                if k != "params":
+                    g[k] = v
+            for p, pid in zip(g["params"], gsd["params"]):
+                s = self.store.slots[self._ptr2name[p.data_ptr()]]
+                st = sd["state"].get(pid)
+                if st:
+                    sl = slice(s.offset, s.offset + s.numel)
+                    self.exp_avg[sl].copy_(st["exp_avg"].reshape(-1))
+                    self.exp_avg_sq[sl].copy_(st["exp_avg_sq"].reshape(-1))
+                    self.steps[gi] = int(float(st["step"]))
+                idx += 1

@@ -1,0 +1,88 @@
+"""Fused AdamW(+SR) and global clip on the GPU vs the oracle restatement (pinned to the reference)."""
+import numpy as np
+import pytest
+import torch
+
+from onetrainer_amd.module.param_store import FlatParamStore
+from onetrainer_amd.util.optimizer.adamw_fused import FusedAdamW
+from oracle import adamw as OA
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [("a", (1000,)), ("b", (37,)), ("c", (64, 70)), ("d", (5,))]
+
+
+def bits(t):
+    return t.detach().cpu().contiguous().view(torch.int16).numpy().astype(np.uint16)
+
+
+@pytest.mark.parametrize("sr", [False, True])
+@pytest.mark.parametrize("clip", [False, True])
+def test_fused_adamw_bitexact(dev, sr, clip):
+    torch.manual_seed(0)
+    st = FlatParamStore([(n, s, "g") for n, s in SHAPES], torch.bfloat16, dev)
+    for n, s in SHAPES:
+        st.params[n].data.copy_(torch.randn(s) * 0.05)
+    opt = FusedAdamW(st, [{"params": [st.params[n] for n, _ in SHAPES]}], lr=1e-3, weight_decay=1e-2,
+                     stochastic_rounding=sr, seed=123)
+    ref = {n: (bits(st.params[n]).reshape(-1), np.zeros(np.prod(s), np.uint16), np.zeros(np.prod(s), np.uint16))
+           for n, s in SHAPES}
+    for step in range(1, 4):
+        for n, s in SHAPES:
+            st.params[n].grad.copy_(torch.randn(s) * 10 ** (-2 + step) * (3 if clip else 1))
+        coef = None
+        if clip:
+            total = opt.clip_grad_norm_(1.0)
+            gl = [bits(st.params[n].grad).reshape(-1) for n, _ in SHAPES]
+            _, tot_ref, coef = OA.clip_grad_norm_bf16(gl, 1.0)
+            assert abs(total.item() - tot_ref) <= 1e-2 * tot_ref
+            assert opt.clip_out[0].item() == coef
+        seed_before = opt.seed
+        opt.step()
+        seed = (seed_before * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
+        for n, s in SHAPES:
+            p, m, v = ref[n]
+            slot = st.slots[n]
+            rand = OA.sr_bits(seed, np.arange(slot.offset, slot.offset + slot.numel)) if sr else None
+            p, m, v = OA.adamw_step_bf16(p, bits(st.params[n].grad).reshape(-1), m, v, step, 1e-3, rand16=rand,
+                                         clip_coef=coef)
+            ref[n] = (p, m, v)
+            assert np.array_equal(bits(opt.exp_avg[slot.offset:slot.offset + slot.numel]), m), (n, step, "m")
+            assert np.array_equal(bits(opt.exp_avg_sq[slot.offset:slot.offset + slot.numel]), v), (n, step, "v")
+            assert np.array_equal(bits(st.params[n]).reshape(-1), p), (n, step, "p")
+
+
+def test_fused_adamw_f32(dev):
+    torch.manual_seed(1)
+    st = FlatParamStore([(n, s, "g") for n, s in SHAPES], torch.float32, dev)
+    for n, s in SHAPES:
+        st.params[n].data.copy_(torch.randn(s) * 0.05)
+    opt = FusedAdamW(st, [{"params": [st.params[n] for n, _ in SHAPES]}], lr=3e-4)
+    ref = {n: (st.params[n].detach().cpu().numpy().reshape(-1).copy(), np.zeros(np.prod(s), np.float32),
+               np.zeros(np.prod(s), np.float32)) for n, s in SHAPES}
+    for step in range(1, 4):
+        for n, s in SHAPES:
+            st.params[n].grad.copy_(torch.randn(s) * 10 ** (-2 + step))
+        opt.step()
+        for n, s in SHAPES:
+            p, m, v = OA.adamw_step_f32(*ref[n][:1], st.params[n].grad.cpu().numpy().reshape(-1), *ref[n][1:], step,
+                                        3e-4)
+            ref[n] = (p, m, v)
+            np.testing.assert_allclose(st.params[n].detach().cpu().numpy().reshape(-1), p, rtol=0, atol=1e-8)
+
+
+def test_state_dict_roundtrip(dev):
+    st = FlatParamStore([(n, s, "g") for n, s in SHAPES], torch.bfloat16, dev)
+    opt = FusedAdamW(st, [{"params": [st.params[n] for n, _ in SHAPES]}], lr=1e-3)
+    for n, s in SHAPES:
+        st.params[n].grad.copy_(torch.randn(s))
+    opt.step()
+    sd = opt.state_dict()
+    assert sd["state"][0]["exp_avg"].shape == (1000,) and float(sd["state"][2]["step"]) == 1.0
+    opt2 = FusedAdamW(st, [{"params": [st.params[n] for n, _ in SHAPES]}], lr=1e-3)
+    opt2.load_state_dict(sd)
+    assert torch.equal(opt2.exp_avg, opt.exp_avg) and opt2.steps == [1]
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: min(1.0, (s + 1) / 10))
+    opt.step()
+    sched.step()
+    assert abs(opt.param_groups[0]["lr"] - 2e-4) < 1e-12
