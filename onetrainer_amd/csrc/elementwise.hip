@@ -253,7 +253,9 @@ OTAMD_API int otamd_colsum(const void* x, long long ldx, int M, int N, int rows_
   const int groups = (M + rows_per_group - 1) / rows_per_group;
   if (hipMemsetAsync(out, 0, sizeof(float) * groups * (long long)N, s) != hipSuccess) return OTAMD_ELAUNCH;
   const int cblocks = (N / 8 + 31) / 32;
-  const int rpb = 512;
+  // enough row blocks to fill the chip (>= ~1024 workgroups), >= 64 rows each
+  int rpb = rows_per_group;
+  while (rpb > 64 && (long long)cblocks * groups * ((rows_per_group + rpb - 1) / rpb) < 1024) rpb = (rpb + 1) / 2;
   const int rblocks = (rows_per_group + rpb - 1) / rpb;
   dim3 grid(cblocks, rblocks, groups);
   colsum_kernel<<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, M, N, rows_per_group, rpb, out);

@@ -429,13 +429,28 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-// sum block partials [nb][2][C] -> dgamma[C], dbeta[C] (fp32)
-__global__ void ln_param_reduce_kernel(const float* __restrict__ part, int nb, int C, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta) {
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < 2 * C; c += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += part[(long long)b * 2 * C + c];
-    if (c < C) dgamma[c] = s; else dbeta[c - C] = s;
+// sum block partials [nb][2][C] -> dgamma[C], dbeta[C] (fp32).  block: 32 columns x 8 partial-lanes
+__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float* __restrict__ part, int nb, int C,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < 2 * C) {
+    int b = pl;
+    for (; b + 8 < nb; b += 16) {
+      s0 += part[(long long)b * 2 * C + c];
+      s1 += part[(long long)(b + 8) * 2 * C + c];
+    }
+    for (; b < nb; b += 8) s0 += part[(long long)b * 2 * C + c];
+  }
+  red[pl][cl] = s0 + s1;
+  __syncthreads();
+  if (pl == 0 && c < 2 * C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
+    if (c < C) dgamma[c] = t; else dbeta[c - C] = t;
   }
 }
 
@@ -459,12 +474,12 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
   if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8 || lddx % 8) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)gamma) & 15) return OTAMD_EINVAL;
   int nb = (rows + 3) / 4;
-  if (nb > 1024) nb = 1024;
+  if (nb > 512) nb = 512;
   ln_bwd_kernel<<<nb, 256, 8 * C * sizeof(float), stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy,
                                                             (bf16_t*)dx, lddx, rows, C, (const bf16_t*)gamma, mean,
                                                             rstd, part, accumulate);
   OTAMD_CHECK_LAUNCH();
-  ln_param_reduce_kernel<<<(2 * C + 255) / 256, 256, 0, stream>>>(part, nb, C, dgamma, dbeta);
+  ln_param_reduce_kernel<<<(2 * C + 31) / 32, 256, 0, stream>>>(part, nb, C, dgamma, dbeta);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
