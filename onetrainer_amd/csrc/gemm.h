@@ -1,0 +1,85 @@
+// Shared GEMM-engine definitions (gemm.hip = 128x128 4-wave kernel, gemm2.hip = 8-wave
+// 256-wide LDS-DMA kernels).  GemmArgs is passed by value to the kernels and through the C ABI.
+#pragma once
+#include "common.h"
+
+enum { OPM_K = 0, OPM_MN = 1, OPM_CONV_FWD = 2, OPM_CONV_DGRAD = 3, OPM_CONV_WGRAD = 4 };
+
+struct ConvGeom {
+  int N;             // batch
+  int SH, SW, SC;    // gathered (source) tensor: spatial dims and channel count
+  int RH, RW;        // spatial dims decoding a GEMM row index (fwd: output, dgrad: input, wgrad: output)
+  int KH, KW, stride, pad;
+  int upsample;      // source read through a virtual nearest-2x upsample (fwd / wgrad)
+  int pad_;
+  long long ld;      // pixel stride of the source, elements
+};
+
+struct GemmArgs {
+  const bf16_t* A; long long lda; int amode;
+  const bf16_t* B; long long ldb; int bmode;
+  void* C; long long ldc; int c_f32; int accumulate;
+  int M, N, K;
+  float alpha;
+  const bf16_t* bias;                                          // + bias[n]
+  const bf16_t* rowvec; long long ldv; int rows_per_vec;       // + rowvec[(m/rows_per_vec)*ldv + n]
+  const bf16_t* residual; long long ldr;                       // + residual[m*ldr + n]
+  float* slab;                                                 // split-K partials [splits][M][N]
+  int k_per_split;
+  ConvGeom ga, gb;
+};
+
+
+// epilogue for 4 consecutive output columns n..n+3 of row m (fp32 accumulators in v[])
+__device__ __forceinline__ void gemm_store4(const GemmArgs& args, int m, int n, float (&v)[4], int split,
+                                            bool use_slab) {
+  if (use_slab) {
+    float* dst = args.slab + ((long long)split * args.M + m) * args.N + n;
+    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) v[t] *= args.alpha;
+  if (args.bias) {
+    const uint2 b = *reinterpret_cast<const uint2*>(args.bias + n);
+    v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+    v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+  }
+  if (args.rowvec) {
+    const uint2 b = *reinterpret_cast<const uint2*>(args.rowvec + (long long)(m / args.rows_per_vec) * args.ldv + n);
+    v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+    v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+  }
+  if (args.residual) {
+    const uint2 b = *reinterpret_cast<const uint2*>(args.residual + (long long)m * args.ldr + n);
+    v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+    v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+  }
+  if (args.c_f32) {
+    float* dst = reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n;
+    if (args.accumulate) { float4 o = *reinterpret_cast<float4*>(dst); v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w; }
+    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
+    if (args.accumulate) {
+      const uint2 o = *reinterpret_cast<const uint2*>(dst);
+      v[0] += __uint_as_float(o.x << 16); v[1] += __uint_as_float(o.x & 0xffff0000u);
+      v[2] += __uint_as_float(o.y << 16); v[3] += __uint_as_float(o.y & 0xffff0000u);
+    }
+    uint2 o;
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(dst) = o;
+  }
+}
+
+// XCD-aware bijective remap of a linear workgroup id (cdna_hip_programming.md §5 T1)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// K-mode LDS image: [rows][64 k], 128-byte rows, 16-byte chunk c of row r stored at c ^ (r & 7)
+__device__ __forceinline__ int kimg_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// MN-mode LDS image: [64 k rows][RB bytes], 32-byte block b of row k stored at b ^ s(k)
+__device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }

@@ -17,33 +17,10 @@
 // MN-contiguous tiles with ds_read_b64_tr_b16 (hardware transpose), both XOR-swizzled
 // to be bank-conflict free.  The MFMA is issued with swapped operands (B-fragment as
 // the MFMA A operand) so each lane ends with 4 consecutive output columns.
-#include "common.h"
+#include "gemm.h"
 
-enum { OPM_K = 0, OPM_MN = 1, OPM_CONV_FWD = 2, OPM_CONV_DGRAD = 3, OPM_CONV_WGRAD = 4 };
-
-struct ConvGeom {
-  int N;             // batch
-  int SH, SW, SC;    // gathered (source) tensor: spatial dims and channel count
-  int RH, RW;        // spatial dims decoding a GEMM row index (fwd: output, dgrad: input, wgrad: output)
-  int KH, KW, stride, pad;
-  int upsample;      // source read through a virtual nearest-2x upsample (fwd / wgrad)
-  int pad_;
-  long long ld;      // pixel stride of the source, elements
-};
-
-struct GemmArgs {
-  const bf16_t* A; long long lda; int amode;
-  const bf16_t* B; long long ldb; int bmode;
-  void* C; long long ldc; int c_f32; int accumulate;
-  int M, N, K;
-  float alpha;
-  const bf16_t* bias;                                          // + bias[n]
-  const bf16_t* rowvec; long long ldv; int rows_per_vec;       // + rowvec[(m/rows_per_vec)*ldv + n]
-  const bf16_t* residual; long long ldr;                       // + residual[m*ldr + n]
-  float* slab;                                                 // split-K partials [splits][M][N]
-  int k_per_split;
-  ConvGeom ga, gb;
-};
+#include <stdlib.h>
+#include <string.h>
 
 #define BM 128
 #define BN 128
@@ -51,10 +28,7 @@ struct GemmArgs {
 #define NTHREADS 256
 
 // --- LDS images ------------------------------------------------------------------------
-// K-mode image: [BMN rows][64 k], 128-byte rows, 16-byte chunk c stored at c ^ (row & 7)
-__device__ __forceinline__ int kimg_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
-// MN-mode image: [64 k rows][128 mn], 256-byte rows, 32-byte block b stored at b ^ s(k)
-__device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+// (K-mode image and the MN-mode swizzle are in gemm.h; v1 MN images have 256-byte rows)
 __device__ __forceinline__ int mnimg_off(int k, int col) {  // col: element index, multiple of 4
   const int blk = col >> 4, within = (col & 15) << 1;
   return k * 256 + ((blk ^ mn_swz(k)) << 5) + within;
@@ -212,11 +186,6 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* img, int mnb, int kb) {
 
 template <int MODE> struct IsK { static constexpr bool v = (MODE == OPM_K || MODE == OPM_CONV_FWD || MODE == OPM_CONV_DGRAD); };
 
-// XCD-aware bijective remap of a linear workgroup id (cdna_hip_programming.md §5 T1)
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-}
 
 template <int AM, int BMODE>
 __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs args) {
@@ -298,44 +267,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs args) {
       const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
       if (n >= args.N) continue;   // N % 4 == 0 is a launcher precondition
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (use_slab) {
-        float* dst = args.slab + ((long long)split * args.M + m) * args.N + n;
-        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-        continue;
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] *= args.alpha;
-      if (args.bias) {
-        const uint2 b = *reinterpret_cast<const uint2*>(args.bias + n);
-        v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
-        v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
-      }
-      if (args.rowvec) {
-        const uint2 b = *reinterpret_cast<const uint2*>(args.rowvec + (long long)(m / args.rows_per_vec) * args.ldv + n);
-        v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
-        v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
-      }
-      if (args.residual) {
-        const uint2 b = *reinterpret_cast<const uint2*>(args.residual + (long long)m * args.ldr + n);
-        v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
-        v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
-      }
-      if (args.c_f32) {
-        float* dst = reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n;
-        if (args.accumulate) { float4 o = *reinterpret_cast<float4*>(dst); v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w; }
-        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
-        if (args.accumulate) {
-          const uint2 o = *reinterpret_cast<const uint2*>(dst);
-          v[0] += __uint_as_float(o.x << 16); v[1] += __uint_as_float(o.x & 0xffff0000u);
-          v[2] += __uint_as_float(o.y << 16); v[3] += __uint_as_float(o.y & 0xffff0000u);
-        }
-        uint2 o;
-        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(dst) = o;
-      }
+      gemm_store4(args, m, n, v, split, use_slab);
     }
   }
 }
@@ -382,6 +314,37 @@ static gemm_fn pick(int am, int bm) {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream);   // gemm2.hip
+
+// tile choice: -1 = v1 128x128 (4 waves), 0 = 256x256, 1 = 256x128, 2 = 128x256 (8 waves, LDS-DMA).
+// Cost model: waves of 256 CUs x tile work / relative per-CU throughput of the tile shape.
+// OTAMD_GEMM_TILE=v1|256x256|256x128|128x256 forces a choice (tests exercise every variant).
+static int choose_tile(int M, int N, int splits) {
+  static int forced = -2;
+  if (forced == -2) {
+    const char* e = getenv("OTAMD_GEMM_TILE");
+    forced = -3;
+    if (e) {
+      if (!strcmp(e, "v1")) forced = -1;
+      else if (!strcmp(e, "256x256")) forced = 0;
+      else if (!strcmp(e, "256x128")) forced = 1;
+      else if (!strcmp(e, "128x256")) forced = 2;
+    }
+  }
+  if (forced != -3) return forced;
+  const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256};
+  const double rate[4] = {0.55, 1.0, 0.85, 0.85};
+  int best = -1;
+  double best_cost = 1e300;
+  for (int t = 0; t < 4; ++t) {
+    const long long tiles = (long long)((M + bm[t] - 1) / bm[t]) * ((N + bn[t] - 1) / bn[t]) * splits;
+    const long long waves = (tiles + 255) / 256;
+    const double cost = (double)waves * bm[t] * bn[t] / rate[t];
+    if (cost < best_cost * 0.999) { best_cost = cost; best = t - 1; }
+  }
+  return best;
+}
+
 // C-ABI.  Preconditions (checked, OTAMD_EINVAL otherwise): M,N,K > 0; N % 4 == 0; K-mode
 // operands need K % 8 == 0, MN-mode operands MN % 8 == 0; leading dims multiples of 8
 // elements; base pointers 16-byte aligned; conv gathers need SC % 8 == 0.
@@ -411,10 +374,16 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
   } else {
     a.slab = nullptr;
   }
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);
-  OTAMD_CHECK_LAUNCH();
+  const int tile = choose_tile(a.M, a.N, splits);
+  int rc = OTAMD_EUNSUPPORTED;
+  if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
+  if (rc == OTAMD_ELAUNCH) return rc;
+  if (rc != OTAMD_OK) {
+    const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    dim3 grid(tiles, 1, splits);
+    hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);
+    OTAMD_CHECK_LAUNCH();
+  }
   if (splits > 1) {
     long long t4 = (long long)a.M * a.N / 4;
     int blocks = (int)std::min<long long>((t4 + 255) / 256, 4096);

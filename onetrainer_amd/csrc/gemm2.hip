@@ -1,0 +1,322 @@
+// bf16 MFMA GEMM engine v2: 8 waves, 256-wide tiles, LDS-DMA staging (gfx950).
+//
+// Same operand modes / epilogues as gemm.hip (see its header for the op -> mode table), but
+// built for the L2->CU bandwidth budget of MI355X: a 128x128 tile needs ~64 B/clk/CU of operand
+// traffic at full MFMA rate, more than the XCD L2 delivers; 256x256 halves it.
+//   * tiles 256x256 (8 waves as 2x4, 128x64 each), 256x128 or 128x256 (8 waves, 64x64 each);
+//   * operands are moved HBM/L2 -> LDS by `buffer_load_dwordx4 ... lds` (LDS-DMA): no VGPR
+//     staging, and the buffer descriptor's range check zero-fills every out-of-range lane, which
+//     is how conv padding / tile tails become zeros;
+//   * LDS images are lane-linear per 1 KiB DMA piece; the XOR swizzles that make ds_read_b128 /
+//     ds_read_b64_tr_b16 bank-conflict free are applied on the SOURCE address (rule 21);
+//   * two LDS stages, raw s_barrier, counted s_waitcnt vmcnt(N): the next tile's DMA stays in
+//     flight across the barrier while the current one is multiplied.
+#include "gemm.h"
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) short4v lds_s4_t;
+#define OFF_INVALID 0x80000000u
+
+#define MEMBAR() asm volatile("" ::: "memory")
+#define BARRIER()                      \
+  do {                                 \
+    MEMBAR();                          \
+    __builtin_amdgcn_s_barrier();      \
+    MEMBAR();                          \
+  } while (0)
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+
+template <int MODE> struct IsKMode {
+  static constexpr bool v = (MODE == OPM_K || MODE == OPM_CONV_FWD || MODE == OPM_CONV_DGRAD);
+};
+
+// Per-lane DMA state of one operand tile (BMN rows/cols x 64 k), NI = BMN/64 pieces per lane.
+template <int MODE, int BMN>
+struct Stage {
+  static constexpr bool KM = IsKMode<MODE>::v;
+  static constexpr int NI = BMN / 64;
+  static constexpr int RB = BMN * 2;      // MN-mode row bytes
+  int a[NI], b[NI], c[NI];                // K: (row elem offset | conv n,y0,x0) ; MN: (k row, col, -)
+  int t0, t1, t2;                         // K: logical chunk ; MN-conv: per-piece decode lives in a/b/c
+  bool ok[NI];
+
+  __device__ __forceinline__ void prepare(const ConvGeom& g, long long ld, int mn0, int MNsz, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = wave + 8 * i;
+      if constexpr (KM) {
+        const int r = 8 * j + (lane >> 3);
+        const int gm = mn0 + r;
+        ok[i] = gm < MNsz;
+        if constexpr (MODE == OPM_K) {
+          a[i] = gm * (int)ld;
+        } else {
+          const int rr = ok[i] ? gm : 0;
+          const int hw = g.RH * g.RW;
+          const int n = rr / hw, rem = rr - n * hw;
+          const int y = rem / g.RW, x = rem - y * g.RW;
+          a[i] = n;
+          if constexpr (MODE == OPM_CONV_FWD) { b[i] = y * g.stride - g.pad; c[i] = x * g.stride - g.pad; }
+          else { b[i] = y + g.pad; c[i] = x + g.pad; }
+        }
+      } else {
+        const int byte = j * 1024 + lane * 16;
+        const int r = byte / RB;
+        const int pc = (byte % RB) >> 4;
+        const int lb = (pc >> 1) ^ mn_swz(r);
+        const int col = mn0 + (lb * 2 + (pc & 1)) * 8;
+        a[i] = r;
+        ok[i] = col < MNsz;
+        if constexpr (MODE == OPM_MN) {
+          b[i] = col;
+        } else {   // OPM_CONV_WGRAD: col = (tap, ch)
+          const int cc = ok[i] ? col : 0;
+          const int tap = cc / g.SC;
+          c[i] = cc - tap * g.SC;
+          b[i] = tap;
+        }
+      }
+    }
+    if constexpr (KM) t0 = (lane & 7) ^ ((lane >> 3) & 7);
+  }
+
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* img, const ConvGeom& g, long long ld, int k0,
+                                        int Kend, int wave) {
+    if constexpr (KM) {
+      const int k = k0 + 8 * t0;
+      const bool kok = k < Kend;
+      int r_ = 0, s_ = 0, ch = 0;
+      if constexpr (MODE != OPM_K) {
+        const int tap = kok ? k / g.SC : 0;
+        ch = k - tap * g.SC;
+        r_ = tap / g.KW;
+        s_ = tap - r_ * g.KW;
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        unsigned off = OFF_INVALID;
+        if constexpr (MODE == OPM_K) {
+          if (kok && ok[i]) off = (unsigned)(a[i] + k) * 2u;
+        } else {
+          bool v = kok && ok[i];
+          int sy, sx;
+          if constexpr (MODE == OPM_CONV_FWD) {
+            const int y = b[i] + r_, x = c[i] + s_;
+            if (g.upsample) { v = v && y >= 0 && y < 2 * g.SH && x >= 0 && x < 2 * g.SW; sy = y >> 1; sx = x >> 1; }
+            else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
+          } else {
+            const int ty = b[i] - r_, tx = c[i] - s_;
+            if (g.stride == 1) { sy = ty; sx = tx; }
+            else {
+              v = v && ty >= 0 && tx >= 0 && (ty % g.stride) == 0 && (tx % g.stride) == 0;
+              sy = ty / g.stride; sx = tx / g.stride;
+            }
+            v = v && sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW;
+          }
+          if (v) off = (unsigned)(((a[i] * g.SH + sy) * g.SW + sx) * (int)g.ld + ch) * 2u;
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(img + (wave + 8 * i) * 1024), 16, (int)off, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int k = k0 + a[i];
+        unsigned off = OFF_INVALID;
+        if constexpr (MODE == OPM_MN) {
+          if (ok[i] && k < Kend) off = (unsigned)(k * (int)ld + b[i]) * 2u;
+        } else {   // conv wgrad: k = output pixel
+          bool v = ok[i] && k < Kend;
+          const int kk = v ? k : 0;
+          const int hw = g.RH * g.RW;
+          const int n = kk / hw, rem = kk - n * hw;
+          const int p = rem / g.RW, q = rem - p * g.RW;
+          const int tr = b[i] / g.KW, ts = b[i] - (b[i] / g.KW) * g.KW;
+          const int y = p * g.stride - g.pad + tr, x = q * g.stride - g.pad + ts;
+          int sy, sx;
+          if (g.upsample) { v = v && y >= 0 && y < 2 * g.SH && x >= 0 && x < 2 * g.SW; sy = y >> 1; sx = x >> 1; }
+          else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
+          if (v) off = (unsigned)(((n * g.SH + sy) * g.SW + sx) * (int)g.ld + c[i]) * 2u;
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(img + (wave + 8 * i) * 1024), 16, (int)off, 0, 0, 0);
+      }
+    }
+  }
+};
+
+// fragment of a 16x16x32 operand: lane holds X[mnb + (lane&15)][kb + 8*(lane>>4) + j]
+__device__ __forceinline__ bf16x8 frag_k2(const char* img, int mnb, int kb) {
+  const int lane = threadIdx.x & 63;
+  const int row = mnb + (lane & 15);
+  return *reinterpret_cast<const bf16x8*>(img + kimg_off(row, (kb >> 3) + (lane >> 4)));
+}
+template <int RB>
+__device__ __forceinline__ int mn_off(int k, int col) {
+  return k * RB + ((((col >> 4)) ^ mn_swz(k)) << 5) + ((col & 15) << 1);
+}
+template <int RB>
+__device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k0 = kb + 8 * g + q;
+  const int col = mnb + 4 * p;
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + mn_off<RB>(k0, col)));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + mn_off<RB>(k0 + 4, col)));
+  short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int AM, int BMODE, int BM, int BN>
+__global__ void __launch_bounds__(512, 2) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int WN = (BM == 256 && BN == 128) ? 2 : 4;
+  constexpr int WM = 8 / WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 16, NJ = TN / 16;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
+  constexpr int STAGE = ABYTES + BBYTES;
+  constexpr int LOADS = BM / 64 + BN / 64;
+  constexpr bool AK = IsKMode<AM>::v, BKm = IsKMode<BMODE>::v;
+
+  const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = wg % tiles_m, tn = wg / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * args.k_per_split;
+  const int kend = min(args.K, kbeg + args.k_per_split);
+  const int nk = (kend - kbeg + 63) / 64;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)args.A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)args.B, (short)0, (int)b_bytes, 0x00020000);
+  Stage<AM, BM> sa;
+  Stage<BMODE, BN> sb;
+  sa.prepare(args.ga, args.lda, m0, args.M, wave, lane);
+  sb.prepare(args.gb, args.ldb, n0, args.N, wave, lane);
+
+  const int wm = wave / WN, wn = wave % WN;
+  float4v acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    sa.issue(ra, smem, args.ga, args.lda, kbeg, kend, wave);
+    sb.issue(rb, smem + ABYTES, args.gb, args.ldb, kbeg, kend, wave);
+  }
+  if (nk > 1) {
+    sa.issue(ra, smem + STAGE, args.ga, args.lda, kbeg + 64, kend, wave);
+    sb.issue(rb, smem + STAGE + ABYTES, args.gb, args.ldb, kbeg + 64, kend, wave);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) wait_vmcnt<LOADS>(); else wait_vmcnt<0>();
+    BARRIER();
+    const char* ia = smem + (kt & 1) * STAGE;
+    const char* ib = ia + ABYTES;
+    // h = 0 fragments, then the h = 1 reads interleaved into the h = 0 MFMA block
+    // (<= 15 LDS reads outstanding so the compiler can count lgkmcnt), then the h = 1 block
+    bf16x8 af0[MI], bf0[NJ], af1[MI], bf1[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf0[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 0) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 0);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af0[i] = AK ? frag_k2(ia, wm * TM + i * 16, 0) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf1[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 32) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 32);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af1[i] = AK ? frag_k2(ia, wm * TM + i * 16, 32) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 32);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf0[j], af0[i], acc[i][j], 0, 0, 0);
+    // interleave: per step 1 LDS read group after every MFMA pair
+#pragma unroll
+    for (int t = 0; t < MI + NJ; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // 2 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, AK && BKm ? 1 : 2, 0);   // DS read(s) of one fragment
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ - 2 * (MI + NJ), 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    BARRIER();
+    if (kt + 2 < nk) {
+      char* nb = smem + (kt & 1) * STAGE;
+      sa.issue(ra, nb, args.ga, args.lda, kbeg + (kt + 2) * 64, kend, wave);
+      sb.issue(rb, nb + ABYTES, args.gb, args.ldb, kbeg + (kt + 2) * 64, kend, wave);
+    }
+  }
+
+  const bool use_slab = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = m0 + wm * TM + i * 16 + (lane & 15);
+    if (m >= args.M) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * TN + j * 16 + 4 * (lane >> 4);
+      if (n >= args.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      gemm_store4(args, m, n, v, split, use_slab);
+    }
+  }
+}
+
+typedef void (*gemm2_fn)(GemmArgs, unsigned, unsigned);
+
+template <int BM, int BN>
+static gemm2_fn pick2(int am, int bm) {
+#define CASE2(a, b) if (am == a && bm == b) return gemm2_kernel<a, b, BM, BN>;
+  CASE2(OPM_K, OPM_K)
+  CASE2(OPM_K, OPM_MN)
+  CASE2(OPM_MN, OPM_MN)
+  CASE2(OPM_MN, OPM_K)
+  CASE2(OPM_CONV_FWD, OPM_K)
+  CASE2(OPM_CONV_DGRAD, OPM_K)
+  CASE2(OPM_MN, OPM_CONV_WGRAD)
+#undef CASE2
+  return nullptr;
+}
+
+// byte extent an operand's gathers may touch (the DMA descriptor's range)
+static long long operand_bytes(int mode, const bf16_t* p, long long ld, int MN, int K, const ConvGeom& g) {
+  (void)p;
+  if (mode == OPM_K) return ((long long)(MN - 1) * ld + K) * 2;
+  if (mode == OPM_MN) return ((long long)(K - 1) * ld + MN) * 2;
+  return ((long long)g.N * g.SH * g.SW - 1) * g.ld * 2 + (long long)g.SC * 2;
+}
+
+// launched by otamd_gemm (gemm.hip) when the v2 tile is selected; returns OTAMD_EUNSUPPORTED
+// when the operand extents do not fit the 31-bit DMA offsets (caller falls back to v1)
+int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
+  const long long ab = operand_bytes(a.amode, a.A, a.lda, a.M, a.K, a.ga);
+  const long long bb = operand_bytes(a.bmode, a.B, a.ldb, a.N, a.K, a.gb);
+  if (ab <= 0 || bb <= 0 || ab >= 0x7fff0000LL || bb >= 0x7fff0000LL) return OTAMD_EUNSUPPORTED;
+  gemm2_fn fn = nullptr;
+  int BMv = 256, BNv = 256;
+  if (tile == 0) fn = pick2<256, 256>(a.amode, a.bmode);
+  else if (tile == 1) { fn = pick2<256, 128>(a.amode, a.bmode); BNv = 128; }
+  else { fn = pick2<128, 256>(a.amode, a.bmode); BMv = 128; }
+  if (!fn) return OTAMD_EUNSUPPORTED;
+  const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
+  const int lds = 2 * (BMv + BNv) * 128;
+  static bool attr_set[3] = {false, false, false};
+  (void)attr_set;
+  hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(fn, dim3(tiles, 1, splits), dim3(512), lds, stream, a, (unsigned)ab, (unsigned)bb);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
