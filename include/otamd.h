@@ -1,0 +1,190 @@
+/* otamd.h -- C ABI of libotamd.so, the MI355X (gfx950) kernels of onetrainer_amd.
+ *
+ * Drop-in boundary for the diffusion train step of OneTrainer (modules/trainer/GenericTrainer.py:672-749
+ * calling modules/modelSetup/<Family>Setup.predict / calculate_loss, loss.backward(), clip_grad_norm_,
+ * optimizer.step()).  The reference is pure Python over diffusers/torch, so every entry point
+ * below replaces an op the reference reaches through those libraries; each cites it.
+ *
+ * Conventions (all launchers):
+ *   - plain device pointers, sizes and strides (in ELEMENTS), bf16 passed as void* (uint16 bits);
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream in the Python host);
+ *   - no implicit allocation: scratch comes in through explicit workspace pointers;
+ *   - return 0 on success, 1 = contract violated (shape / alignment; nothing launched),
+ *     2 = launch error, 3 = unsupported configuration.  Python maps non-zero to RuntimeError;
+ *   - thread-compatible; no global mutable state besides per-process tile-choice caching.
+ * Layouts: activations NHWC (pixels x channels) / token-major [B, N, C]; conv weights
+ * [Cout][kh][kw][Cin]; Linear weights [out][in]; attention Q/K/V/O [B, N, H*D] with strides.
+ */
+#ifndef OTAMD_H
+#define OTAMD_H
+#include <hip/hip_runtime.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { OTAMD_OK = 0, OTAMD_EINVAL = 1, OTAMD_ELAUNCH = 2, OTAMD_EUNSUPPORTED = 3 };
+
+/* GEMM operand modes */
+enum { OPM_K = 0, OPM_MN = 1, OPM_CONV_FWD = 2, OPM_CONV_DGRAD = 3, OPM_CONV_WGRAD = 4 };
+
+typedef struct ConvGeom {
+  int N, SH, SW, SC, RH, RW, KH, KW, stride, pad, upsample, pad_;
+  long long ld;
+} ConvGeom;
+
+/* C[M,N] = alpha * op(A) op(B) (+bias[n]) (+rowvec[m/rows_per_vec][n]) (+residual[m][n]) (+C if accumulate) */
+typedef struct GemmArgs {
+  const void* A; long long lda; int amode;
+  const void* B; long long ldb; int bmode;
+  void* C; long long ldc; int c_f32; int accumulate;
+  int M, N, K;
+  float alpha;
+  const void* bias;
+  const void* rowvec; long long ldv; int rows_per_vec;
+  const void* residual; long long ldr;
+  float* slab;
+  int k_per_split;
+  ConvGeom ga, gb;
+} GemmArgs;
+
+typedef struct AttnArgs {
+  const void *q, *k, *v; void* o; float* lse;
+  const void* dout; const float* delta; void *dq, *dk, *dv; float *dk32, *dv32;
+  long long ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;
+  long long bsq, bsk, bsv, bso, bsdo, bsdq, bsdk, bsdv;
+  int B, H, Nq, Nk, Dv;
+  float scale;
+  int qsplit, pad_;
+} AttnArgs;
+
+typedef struct AdamwGroup {
+  long long begin, end;
+  float wd_factor, one_minus_beta1, beta2, one_minus_beta2, bc2_sqrt, eps, neg_step_size, pad;
+} AdamwGroup;
+
+typedef struct NormChunk { long long begin, end; int tensor, pad; } NormChunk;
+
+/* replaces: diffusers Linear/Conv2d fwd+bwd inside model.unet(...) (modules/modelSetup/BaseStableDiffusionXLSetup.py:268-273); conv/linear dgrad/wgrad of loss.backward() (modules/trainer/GenericTrainer.py:693-696) */
+int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_bytes, hipStream_t stream);
+
+/* replaces: ABI check */
+int otamd_gemm_args_size(void);
+
+/* replaces: ABI check */
+int otamd_conv_geom_size(void);
+
+/* replaces: F.scaled_dot_product_attention in diffusers Attention (attn1/attn2 of every BasicTransformerBlock) */
+int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream);
+
+/* replaces: autograd of scaled_dot_product_attention (GenericTrainer.py:693-696) */
+int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream);
+
+/* replaces: ABI check */
+int otamd_attn_args_size(void);
+
+/* replaces: ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out (diffusers, via BaseStableDiffusionXLSetup.py:268-273) */
+int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long long ldy, int N, int HW, int C, int G,
+    float eps, const void* gamma, const void* beta, int silu, float* mean, float* rstd, float* a, float* b,
+    double* ws, hipStream_t stream);
+
+/* replaces: autograd of GroupNorm(+SiLU) */
+int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long
+    lddx, int N, int HW, int C, int G, const void* gamma, int silu, const float* mean, const float* rstd,
+    const float* a, const float* b, void* dgamma, void* dbeta, int param_f32, int param_acc, double* ws,
+    float* fws, int accumulate, hipStream_t stream);
+
+/* replaces: BasicTransformerBlock norm1/norm2/norm3 */
+int otamd_layernorm_fwd(const void* x, long long ldx, void* y, long long ldy, int rows, int C, float eps,
+    const void* gamma, const void* beta, float* mean, float* rstd, hipStream_t stream);
+
+/* replaces: autograd of LayerNorm */
+int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long
+    lddx, int rows, int C, const void* gamma, const float* mean, const float* rstd, void* dgamma, void* dbeta,
+    int param_f32, int param_acc, float* part, int accumulate, hipStream_t stream);
+
+/* replaces: diffusers GEGLU (ff.net.0) hidden * gelu(gate) */
+int otamd_geglu_fwd(const void* h, long long ldh, void* out, long long ldo, int M, int F, hipStream_t s);
+
+/* replaces: autograd of GEGLU */
+int otamd_geglu_bwd(const void* h, long long ldh, const void* dout, long long lddo, void* dh, long long lddh,
+    int M, int F, hipStream_t s);
+
+/* replaces: nonlinearity(temb) / TimestepEmbedding act */
+int otamd_silu_fwd(const void* x, void* y, long long n, hipStream_t s);
+
+/* replaces: autograd of SiLU */
+int otamd_silu_bwd(const void* x, const void* dy, void* dx, long long n, hipStream_t s);
+
+/* replaces: torch.cat([hidden, res_hidden], dim=1) in up blocks */
+int otamd_concat_channels(const void* a, long long lda, int Ca, const void* b, long long ldb, int Cb, void*
+    out, long long P, hipStream_t s);
+
+/* replaces: autograd of F.interpolate(scale_factor=2, nearest) in Upsample2D */
+int otamd_upsample2x_bwd(const void* dup, void* dx, int N, int H, int W, int C, int accumulate, hipStream_t
+    s);
+
+/* replaces: bias / time_emb_proj gradients (autograd of Linear/Conv2d bias, temb broadcast add) */
+int otamd_colsum(const void* x, long long ldx, int M, int N, int rows_per_group, void* out, int out_f32, int
+    accumulate, float* ws, long long ws_floats, hipStream_t s);
+
+/* replaces: workspace size query for otamd_colsum */
+long long otamd_colsum_ws_floats(int M, int N, int rows_per_group);
+
+/* replaces: weight layout transform for conv dgrad (no reference equivalent; internal) */
+int otamd_conv_weight_transpose(const void* w, void* wt, int Cout, int KK, int Cin, hipStream_t s);
+
+/* replaces: fp32 reduction result -> bf16/f32 grad (internal) */
+int otamd_cast_f32(const float* x, void* y, long long n, int dst_f32, int accumulate, hipStream_t s);
+
+/* replaces: diffusers get_timestep_embedding (UNet time_proj / add_time_proj) */
+int otamd_timestep_embedding(const float* t, int n, int dim, void* out, long long ldo, hipStream_t s);
+
+/* replaces: residual add where not fused into a GEMM epilogue */
+int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s);
+
+/* replaces: ModelSetupNoiseMixin._create_noise (modules/modelSetup/mixin/ModelSetupNoiseMixin.py:18-49) */
+int otamd_noise(void* out, int f32, long long n, long long offset, unsigned long long seed, hipStream_t s);
+
+/* replaces: ModelSetupNoiseMixin._get_timestep_discrete (ModelSetupNoiseMixin.py:51-155) */
+int otamd_timesteps(int* out, int n, long long sample0, unsigned long long seed, int dist, int
+    num_train_timesteps, float min_s, float max_s, float shift, float bias, float weight, hipStream_t s);
+
+/* replaces: BaseStableDiffusionXLSetup.predict scale + _add_noise_discrete + get_velocity (BaseStableDiffusionXLSetup.py:214-236,277-291; ModelSetupDiffusionMixin.py:15-38) */
+int otamd_ddpm_prologue(const void* latent, const void* noise, int lat_f32, const int* timestep, const float*
+    acp, const float* sqrt_acp, const float* sqrt_1m, float sf, int B, long long HW, int C, int cpad, void*
+    unet_in, void* target, int target_kind, float* scaled_out, hipStream_t s);
+
+/* replaces: BaseFluxSetup.predict scale/shift + ModelSetupFlowMatchingMixin._add_noise_discrete (ModelSetupFlowMatchingMixin.py:14-39) + flow target (BaseFluxSetup.py:307) */
+int otamd_flow_prologue(const void* latent, const void* noise, int lat_f32, const int* timestep, float sf,
+    float shift_factor, int num_t, int B, long long HW, int C, int cpad, void* model_in, void* target,
+    hipStream_t s);
+
+/* replaces: ModelSetupDiffusionLossMixin._diffusion_losses/__unmasked_losses + .mean() (ModelSetupDiffusionLossMixin.py:119-168,233-279; BaseStableDiffusionXLSetup.py:360-373) */
+int otamd_mse_loss(const void* pred, int cpad, const void* target, int tgt_f32, int B, long long HW, int C,
+    float mse_strength, float scale, const float* loss_weight, const int* timestep, const float* sqrt_acp,
+    const float* sqrt_1m, int loss_fn, float gamma, int v_pred, float ga, float* ws, long long ws_floats,
+    float* loss_out, float* coef, float* losses_out, hipStream_t s);
+
+/* replaces: autograd of the MSE loss */
+int otamd_mse_grad(const void* pred, int cpad, const void* target, int tgt_f32, int B, long long HW, int C,
+    const float* coef, const float* grad_out, void* dpred, hipStream_t s);
+
+/* replaces: AdamW step_adamw_parameter + addcdiv_stochastic_ (modules/util/optimizer/adamw_extensions.py:17-150; modules/util/bf16_stochastic_rounding.py:5-61), patched at modules/util/create.py:509-534 */
+int otamd_adamw_bf16(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups, int
+    n_groups, const float* clip_coef, int stochastic_rounding, unsigned long long seed, hipStream_t stream);
+
+/* replaces: same, fp32 parameters (LoRA weights, TrainConfig.py:959) */
+int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups, int
+    n_groups, const float* clip_coef, hipStream_t stream);
+
+/* replaces: nn.utils.clip_grad_norm_(parameters, clip_grad_norm) (modules/trainer/GenericTrainer.py:712-713) */
+int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void* chunks, int n_chunks, double*
+    tensor_sq, int n_tensors, float max_norm, float* out, hipStream_t stream);
+
+/* replaces: the grad scaling half of clip_grad_norm_ when not fused into AdamW */
+int otamd_scale_bf16_by_device_scalar(void* g, long long n, const float* coef, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OTAMD_H */

@@ -68,9 +68,9 @@ SIGNATURES: dict[str, list] = {
     "otamd_scale_bf16_by_device_scalar": [VP, LL, VP, VP],
     # norm.hip
     "otamd_groupnorm_fwd": [VP, LL, VP, LL, I, I, I, I, F, VP, VP, I, VP, VP, VP, VP, VP, VP],
-    "otamd_groupnorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, I, I, VP, I, VP, VP, VP, VP, VP, VP, VP, VP, I, VP],
+    "otamd_groupnorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, I, I, VP, I, VP, VP, VP, VP, VP, VP, I, I, VP, VP, I, VP],
     "otamd_layernorm_fwd": [VP, LL, VP, LL, I, I, F, VP, VP, VP, VP, VP],
-    "otamd_layernorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, VP, I, VP],
+    "otamd_layernorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],
     # attention.hip
     "otamd_attn_args_size": [],
     "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],
@@ -82,7 +82,8 @@ SIGNATURES: dict[str, list] = {
     "otamd_silu_bwd": [VP, VP, VP, LL, VP],
     "otamd_concat_channels": [VP, LL, I, VP, LL, I, VP, LL, VP],
     "otamd_upsample2x_bwd": [VP, VP, I, I, I, I, I, VP],
-    "otamd_colsum": [VP, LL, I, I, I, VP, VP],
+    "otamd_colsum": [VP, LL, I, I, I, VP, I, I, VP, LL, VP],
+    "otamd_colsum_ws_floats": [I, I, I],
     "otamd_conv_weight_transpose": [VP, VP, I, I, I, VP],
     "otamd_cast_f32": [VP, VP, LL, I, I, VP],
     "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
@@ -110,7 +111,7 @@ def lib():
         for name, args in SIGNATURES.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = C.c_int
+            fn.restype = C.c_longlong if name.endswith("_ws_floats") else C.c_int
         _lib = L
     return _lib
 

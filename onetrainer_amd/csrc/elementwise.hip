@@ -113,16 +113,17 @@ __global__ void upsample_bwd_kernel(const bf16_t* __restrict__ dup, bf16_t* __re
   }
 }
 
-// out[g, n] (fp32) = sum_{m in group g} x[m, n];  rows_per_group rows per group; grid (ceil(N/256)... )
-// block: 256 threads = 32 column-chunks(8 cols) x 8 row-lanes
-__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, long long ldx, int M, int N,
-                                                     int rows_per_group, int rows_per_block, float* __restrict__ out) {
-  __shared__ float red[8][256 + 8];
+// column sums per row group, two deterministic passes (no atomics, no memset):
+//   pass 1: ws[g][rb][n] = sum of rows [rb*rpb, (rb+1)*rpb) of group g   (block: 32 col-chunks x 8 row-lanes)
+//   pass 2: out[g][n] (bf16 or f32, optionally accumulated) = sum_rb ws[g][rb][n]
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16_t* __restrict__ x, long long ldx, int M, int N,
+                                                             int rows_per_group, int rpb, int RB, float* __restrict__ ws) {
+  __shared__ float red[8][256 + 4];
   const int cchunk = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int col = (blockIdx.x * 32 + cchunk) * 8;
-  const int g = blockIdx.z;
-  const int r0 = g * rows_per_group + blockIdx.y * rows_per_block;
-  const int r1 = min(min(M, (g + 1) * rows_per_group), r0 + rows_per_block);
+  const int g = blockIdx.z, rb = blockIdx.y;
+  const int r0 = g * rows_per_group + rb * rpb;
+  const int r1 = min(min(M, (g + 1) * rows_per_group), r0 + rpb);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (col < N) {
     for (int m = r0 + rl; m < r1; m += 8) {
@@ -135,12 +136,27 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[rl][cchunk * 8 + j] = s[j];
   __syncthreads();
-  if (rl == 0 && col < N) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) {
+    float t = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = 0.f;
-      for (int k = 0; k < 8; ++k) t += red[k][cchunk * 8 + j];
-      atomicAdd(&out[(long long)g * N + col + j], t);
+    for (int k = 0; k < 8; ++k) t += red[k][threadIdx.x];
+    ws[((long long)g * RB + rb) * N + c] = t;
+  }
+}
+__global__ void colsum_reduce_kernel(const float* __restrict__ ws, int RB, int N, int groups, void* __restrict__ out,
+                                     int out_f32, int acc) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)groups * N;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long g = i / N, n = i - g * N;
+    float t = 0.f;
+    for (int rb = 0; rb < RB; ++rb) t += ws[(g * RB + rb) * N + n];
+    if (out_f32) {
+      float* d = reinterpret_cast<float*>(out) + i;
+      *d = acc ? *d + t : t;
+    } else {
+      bf16_t* d = reinterpret_cast<bf16_t*>(out) + i;
+      *d = f2bf(acc ? bf2f(*d) + t : t);
     }
   }
 }
@@ -247,18 +263,29 @@ OTAMD_API int otamd_upsample2x_bwd(const void* dup, void* dx, int N, int H, int 
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
-// out: fp32 [groups][N], zeroed here
-OTAMD_API int otamd_colsum(const void* x, long long ldx, int M, int N, int rows_per_group, float* out, hipStream_t s) {
-  if (!x || !out || M <= 0 || N % 8 || ldx % 8 || rows_per_group <= 0 || !al16(x)) return OTAMD_EINVAL;
-  const int groups = (M + rows_per_group - 1) / rows_per_group;
-  if (hipMemsetAsync(out, 0, sizeof(float) * groups * (long long)N, s) != hipSuccess) return OTAMD_ELAUNCH;
-  const int cblocks = (N / 8 + 31) / 32;
-  // enough row blocks to fill the chip (>= ~1024 workgroups), >= 64 rows each
+// out: [groups][N] bf16 (out_f32=0) or f32; ws: >= groups * RB * N floats where RB = colsum_row_blocks(...)
+static int colsum_rpb(int rows_per_group, int N, int groups) {
+  const int cblocks = (N + 255) / 256;
   int rpb = rows_per_group;
   while (rpb > 64 && (long long)cblocks * groups * ((rows_per_group + rpb - 1) / rpb) < 1024) rpb = (rpb + 1) / 2;
-  const int rblocks = (rows_per_group + rpb - 1) / rpb;
-  dim3 grid(cblocks, rblocks, groups);
-  colsum_kernel<<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, M, N, rows_per_group, rpb, out);
+  return rpb;
+}
+OTAMD_API long long otamd_colsum_ws_floats(int M, int N, int rows_per_group) {
+  const int groups = (M + rows_per_group - 1) / rows_per_group;
+  const int rpb = colsum_rpb(rows_per_group, N, groups);
+  return (long long)groups * ((rows_per_group + rpb - 1) / rpb) * N;
+}
+OTAMD_API int otamd_colsum(const void* x, long long ldx, int M, int N, int rows_per_group, void* out, int out_f32,
+                           int accumulate, float* ws, long long ws_floats, hipStream_t s) {
+  if (!x || !out || !ws || M <= 0 || N % 8 || ldx % 8 || rows_per_group <= 0 || !al16(x)) return OTAMD_EINVAL;
+  const int groups = (M + rows_per_group - 1) / rows_per_group;
+  const int rpb = colsum_rpb(rows_per_group, N, groups);
+  const int RB = (rows_per_group + rpb - 1) / rpb;
+  if (ws_floats < (long long)groups * RB * N) return OTAMD_EINVAL;
+  dim3 grid((N + 255) / 256, RB, groups);
+  colsum_partial_kernel<<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, M, N, rows_per_group, rpb, RB, ws);
+  OTAMD_CHECK_LAUNCH();
+  colsum_reduce_kernel<<<grid_for((long long)groups * N), 256, 0, s>>>(ws, RB, N, groups, out, out_f32, accumulate);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

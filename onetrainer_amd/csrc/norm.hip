@@ -12,6 +12,8 @@
 // writes dx once.
 #include "common.h"
 
+__device__ __forceinline__ void store_param_grad(void* p, long long i, float v, int f32, int acc);
+
 // ------------------------------------------------------------------------------------------
 // per-(n, c) partial sums of x and x^2, accumulated in double via atomics
 // grid: (pixel blocks, N); block 256 threads; thread t owns channel chunk t % C8 and pixels
@@ -175,7 +177,8 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const bf16_t* __rest
 // per-(n,g) constants c1 = sum_c gamma_c S1 / cnt, c2 = sum_c gamma_c S2 / cnt; also dgamma/dbeta
 __global__ void gn_bwd_finalize_kernel(const double* __restrict__ s1, const double* __restrict__ s2, int N, int HW,
                                        int C, int G, const bf16_t* __restrict__ gamma, float* __restrict__ c1,
-                                       float* __restrict__ c2, float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                       float* __restrict__ c2, void* __restrict__ dgamma, void* __restrict__ dbeta,
+                                       int pf32, int pacc) {
   const int Cg = C / G;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N * G; i += gridDim.x * blockDim.x) {
     const int n = i / G, g = i - n * G;
@@ -192,8 +195,8 @@ __global__ void gn_bwd_finalize_kernel(const double* __restrict__ s1, const doub
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     double dg = 0, db = 0;
     for (int n = 0; n < N; ++n) { dg += s2[(long long)n * C + c]; db += s1[(long long)n * C + c]; }
-    if (dgamma) dgamma[c] = (float)dg;
-    if (dbeta) dbeta[c] = (float)db;
+    if (dgamma) store_param_grad(dgamma, c, (float)dg, pf32, pacc);
+    if (dbeta) store_param_grad(dbeta, c, (float)db, pf32, pacc);
   }
 }
 
@@ -266,8 +269,8 @@ OTAMD_API int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long lo
 OTAMD_API int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx,
                                   long long lddx, int N, int HW, int C, int G, const void* gamma, int silu,
                                   const float* mean, const float* rstd, const float* a, const float* b,
-                                  float* dgamma, float* dbeta, double* ws, float* fws, int accumulate,
-                                  hipStream_t stream) {
+                                  void* dgamma, void* dbeta, int param_f32, int param_acc, double* ws, float* fws,
+                                  int accumulate, hipStream_t stream) {
   if (!x || !dy || !dx || !mean || !rstd || !a || !b || !ws || !fws || N <= 0 || HW <= 0) return OTAMD_EINVAL;
   if (C % 8 || C % G || ldx % 8 || lddy % 8 || lddx % 8 || C > 8192) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) return OTAMD_EINVAL;
@@ -285,7 +288,8 @@ OTAMD_API int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, 
   OTAMD_CHECK_LAUNCH();
   float* c1 = fws;
   float* c2 = fws + N * G;
-  gn_bwd_finalize_kernel<<<8, 256, 0, stream>>>(s1, s2, N, HW, C, G, (const bf16_t*)gamma, c1, c2, dgamma, dbeta);
+  gn_bwd_finalize_kernel<<<8, 256, 0, stream>>>(s1, s2, N, HW, C, G, (const bf16_t*)gamma, c1, c2, dgamma, dbeta,
+                                                param_f32, param_acc);
   OTAMD_CHECK_LAUNCH();
   const long long chunks = (long long)N * HW * (C / 8);
   if (silu)
@@ -430,8 +434,14 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
 }
 
 // sum block partials [nb][2][C] -> dgamma[C], dbeta[C] (fp32).  block: 32 columns x 8 partial-lanes
+__device__ __forceinline__ void store_param_grad(void* p, long long i, float v, int f32, int acc) {
+  if (f32) { float* d = reinterpret_cast<float*>(p) + i; *d = acc ? *d + v : v; }
+  else { bf16_t* d = reinterpret_cast<bf16_t*>(p) + i; *d = f2bf(acc ? bf2f(*d) + v : v); }
+}
+
 __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float* __restrict__ part, int nb, int C,
-                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                              void* __restrict__ dgamma, void* __restrict__ dbeta,
+                                                              int pf32, int pacc) {
   __shared__ float red[8][33];
   const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -450,7 +460,7 @@ __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float* __res
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += red[k][cl];
-    if (c < C) dgamma[c] = t; else dbeta[c - C] = t;
+    if (c < C) store_param_grad(dgamma, c, t, pf32, pacc); else store_param_grad(dbeta, c - C, t, pf32, pacc);
   }
 }
 
@@ -468,8 +478,8 @@ OTAMD_API int otamd_layernorm_fwd(const void* x, long long ldx, void* y, long lo
 // part: float scratch >= 1024 * 2 * C
 OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx,
                                   long long lddx, int rows, int C, const void* gamma, const float* mean,
-                                  const float* rstd, float* dgamma, float* dbeta, float* part, int accumulate,
-                                  hipStream_t stream) {
+                                  const float* rstd, void* dgamma, void* dbeta, int param_f32, int param_acc,
+                                  float* part, int accumulate, hipStream_t stream) {
   if (!x || !dy || !dx || !gamma || !mean || !rstd || !dgamma || !dbeta || !part) return OTAMD_EINVAL;
   if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8 || lddx % 8) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)gamma) & 15) return OTAMD_EINVAL;
@@ -479,7 +489,7 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
                                                             (bf16_t*)dx, lddx, rows, C, (const bf16_t*)gamma, mean,
                                                             rstd, part, accumulate);
   OTAMD_CHECK_LAUNCH();
-  ln_param_reduce_kernel<<<(2 * C + 31) / 32, 256, 0, stream>>>(part, nb, C, dgamma, dbeta);
+  ln_param_reduce_kernel<<<(2 * C + 31) / 32, 256, 0, stream>>>(part, nb, C, dgamma, dbeta, param_f32, param_acc);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

@@ -310,7 +310,9 @@ def groupnorm_fwd(x, gamma, beta, groups, eps, silu, out=None):
     return out, (mean, rstd, a, b)
 
 
-def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, need_param_grads=True):
+def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, need_param_grads=True,
+                  dgamma=None, dbeta=None, param_acc=False):
+    """returns (dx, dgamma, dbeta); pass dgamma/dbeta (bf16 or f32 grad views) to write them in place."""
     N = x.shape[0]
     _, C_, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
@@ -320,13 +322,15 @@ def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, 
     _, _, lddx = _rows2d(dx)
     mean, rstd, a, b = stats
     dev = x.device
-    dgamma = torch.empty(C_, dtype=F32, device=dev) if need_param_grads else None
-    dbeta = torch.empty(C_, dtype=F32, device=dev) if need_param_grads else None
+    if dgamma is None and need_param_grads:
+        dgamma = torch.empty(C_, dtype=F32, device=dev)
+        dbeta = torch.empty(C_, dtype=F32, device=dev)
+    pf32 = int(dgamma is not None and dgamma.dtype == F32)
     ws = workspace(16 * N * C_ + 8 * N * groups + 64, dev)
     fws = ws[16 * N * C_:].view(torch.float32)
     check(lib().otamd_groupnorm_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, N, HW, C_, groups, _p(gamma), int(silu),
-                                    _p(mean), _p(rstd), _p(a), _p(b), _p(dgamma), _p(dbeta), _p(ws), _p(fws),
-                                    int(accumulate), stream_handle()), "otamd_groupnorm_bwd")
+                                    _p(mean), _p(rstd), _p(a), _p(b), _p(dgamma), _p(dbeta), pf32, int(param_acc),
+                                    _p(ws), _p(fws), int(accumulate), stream_handle()), "otamd_groupnorm_bwd")
     return dx, dgamma, dbeta
 
 
@@ -342,19 +346,20 @@ def layernorm_fwd(x, gamma, beta, eps, out=None):
     return out, (mean, rstd)
 
 
-def layernorm_bwd(x, dy, gamma, stats, dx=None, accumulate=False):
+def layernorm_bwd(x, dy, gamma, stats, dx=None, accumulate=False, dgamma=None, dbeta=None, param_acc=False):
     rows, C_, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
     if dx is None:
         dx = torch.empty(x.shape, dtype=BF16, device=x.device)
     _, _, lddx = _rows2d(dx)
-    dgamma = torch.empty(C_, dtype=F32, device=x.device)
-    dbeta = torch.empty(C_, dtype=F32, device=x.device)
+    if dgamma is None:
+        dgamma = torch.empty(C_, dtype=F32, device=x.device)
+        dbeta = torch.empty(C_, dtype=F32, device=x.device)
     part = workspace(1024 * 2 * C_ * 4, x.device)
     mean, rstd = stats
     check(lib().otamd_layernorm_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, rows, C_, _p(gamma), _p(mean), _p(rstd),
-                                    _p(dgamma), _p(dbeta), _p(part), int(accumulate), stream_handle()),
-          "otamd_layernorm_bwd")
+                                    _p(dgamma), _p(dbeta), int(dgamma.dtype == F32), int(param_acc), _p(part),
+                                    int(accumulate), stream_handle()), "otamd_layernorm_bwd")
     return dx, dgamma, dbeta
 
 
@@ -475,13 +480,19 @@ def upsample2x_bwd(dup, out=None, accumulate=False):
     return out
 
 
-def colsum(x, rows_per_group=None):
-    """fp32 [groups, C] column sums of a [rows, C] view (groups of rows_per_group rows)."""
+def colsum(x, rows_per_group=None, out=None, accumulate=False):
+    """[groups, C] column sums of a [rows, C] view (groups of rows_per_group rows); fp32 unless `out`
+    (bf16 or f32, e.g. a bias-grad view) is given; accumulate adds into `out`."""
     rows, C_, ldx = _rows2d(x)
     rpg = rows if rows_per_group is None else rows_per_group
     groups = (rows + rpg - 1) // rpg
-    out = torch.empty((groups, C_), dtype=F32, device=x.device)
-    check(lib().otamd_colsum(_p(x), ldx, rows, C_, rpg, _p(out), stream_handle()), "otamd_colsum")
+    if out is None:
+        out = torch.empty((groups, C_), dtype=F32, device=x.device)
+    _req(out.numel() == groups * C_ and out.is_contiguous() and out.dtype in (BF16, F32), "colsum out")
+    wsf = lib().otamd_colsum_ws_floats(rows, C_, rpg)
+    ws = workspace(wsf * 4, x.device)
+    check(lib().otamd_colsum(_p(x), ldx, rows, C_, rpg, _p(out), int(out.dtype == F32), int(accumulate), _p(ws), wsf,
+                             stream_handle()), "otamd_colsum")
     return out
 
 

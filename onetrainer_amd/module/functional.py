@@ -82,7 +82,8 @@ class LinearFn(torch.autograd.Function):
         K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
         wref.done()
         if bref is not None:
-            bref.write_f32(K.colsum(dy2))
+            K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
+            bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, dres) + (None,) * (len(ctx.needs_input_grad) - 4)
 
@@ -125,12 +126,11 @@ class ConvFn(torch.autograd.Function):
         drow = None
         P, Q = dy.shape[1], dy.shape[2]
         if ctx.has_rowvec:
-            per = K.colsum(dy, rows_per_group=P * Q)           # [N, Cout] fp32
-            drow = K.cast_f32_bf16(per.contiguous())
-            if bref is not None:
-                bref.write_f32(K.colsum(dy))
-        elif bref is not None:
-            bref.write_f32(K.colsum(dy))
+            drow = K.colsum(dy, rows_per_group=P * Q, out=torch.empty((dy.shape[0], dy.shape[3]), dtype=torch.bfloat16,
+                                                                       device=dy.device))
+        if bref is not None:
+            K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
+            bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, drow, dres, None, None) + (None,) * (len(ctx.needs_input_grad) - 7)
 
@@ -150,9 +150,10 @@ class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, *stats = ctx.saved_tensors
-        dx, dg, db = K.groupnorm_bwd(x, dy, ctx.gref.w, ctx.groups, ctx.silu, stats)
-        ctx.gref.write_f32(dg)
-        ctx.bref.write_f32(db)
+        dx, _, _ = K.groupnorm_bwd(x, dy, ctx.gref.w, ctx.groups, ctx.silu, stats, dgamma=ctx.gref.g,
+                                   dbeta=ctx.bref.g, param_acc=ctx.gref.acc())
+        ctx.gref.done()
+        ctx.bref.done()
         return (dx if ctx.needs_input_grad[0] else None,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
 
@@ -173,9 +174,10 @@ class LayerNormFn(torch.autograd.Function):
         x, *stats = ctx.saved_tensors
         if dy.stride(-1) != 1:
             dy = dy.contiguous()
-        dx, dg, db = K.layernorm_bwd(x, dy, ctx.gref.w, stats)
-        ctx.gref.write_f32(dg)
-        ctx.bref.write_f32(db)
+        dx, _, _ = K.layernorm_bwd(x, dy, ctx.gref.w, stats, dgamma=ctx.gref.g, dbeta=ctx.bref.g,
+                                   param_acc=ctx.gref.acc())
+        ctx.gref.done()
+        ctx.bref.done()
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
 

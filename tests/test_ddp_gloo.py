@@ -1,0 +1,80 @@
+"""Data-parallel gradient reduction (trainer/ddp.py) with world_size 2 over gloo on CPU:
+buckets launch as their parameters become ready (in reverse layout order, as backward produces
+them) and the result equals the sum over ranks (the 1/world factor lives in the loss gradient)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from onetrainer_amd.module.param_store import FlatParamStore
+from onetrainer_amd.trainer.ddp import GradBucketReducer
+
+SPECS = [(f"p{i}", (37 * (i + 1) % 300 + 8,), "g") for i in range(40)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = FlatParamStore(SPECS, torch.float32, "cpu")
+        red = GradBucketReducer(st, bucket_bytes=2048)
+        assert len(red.buckets) > 3
+        launched = []
+        for step in range(2):
+            for i, (n, s, _) in enumerate(SPECS):
+                st.params[n].grad.fill_(rank + 1 + i + 100 * step)
+            for n in reversed(st.order):         # backward finishes parameters in reverse order
+                st.mark_ready([n])
+                launched.append(len(red.works))
+            red.finish()
+            for i, (n, s, _) in enumerate(SPECS):
+                exp = sum(r + 1 + i + 100 * step for r in range(world))
+                assert torch.all(st.params[n].grad == exp), (n, st.params[n].grad[:3], exp)
+        # buckets were issued progressively during "backward", not all at the end
+        assert launched[len(launched) // 4] > 0
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_allreduce_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res
+
+
+def test_bucket_partition_is_contiguous_and_complete():
+    st = FlatParamStore(SPECS, torch.bfloat16, "cpu")
+    if not dist.is_available():
+        pytest.skip("torch.distributed unavailable")
+    red = GradBucketReducer.__new__(GradBucketReducer)
+    GradBucketReducer.__init__(red, st, bucket_bytes=1024)
+    names = [n for b in red.buckets for n in b[2]]
+    assert sorted(names) == sorted(st.order)
+    prev_begin = None
+    for b, e, ns in red.buckets:
+        assert b < e and b == st.slots[ns[-1]].offset
+        if prev_begin is not None:
+            assert e <= prev_begin + 8
+        prev_begin = b

@@ -1,0 +1,94 @@
+"""Host-side logic on CPU: LR schedule vs the reference's own values, config loading, flat store,
+UNet parameter graph vs the oracle and the known SD/SDXL sizes, FLOP counter."""
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from onetrainer_amd.module import unet as U
+from onetrainer_amd.module.param_store import FlatParamStore
+from onetrainer_amd.util import lr_scheduler_util as L
+from onetrainer_amd.util.config.TrainConfig import TrainConfig
+from oracle import unet as OU
+
+G = np.load(Path(__file__).parent / "golden" / "reference_math.npz")
+
+
+@pytest.mark.parametrize("name,fn", [
+    ("constant", L.lr_lambda_warmup(200, L.lr_lambda_constant())),
+    ("cosine", L.lr_lambda_warmup(50, L.lr_lambda_cosine(300))),
+    ("linear", L.lr_lambda_warmup(10, L.lr_lambda_linear(390)))])
+def test_lr_lambdas_match_reference(name, fn):
+    got = np.array([fn(s) for s in range(400)], dtype=np.float64)
+    np.testing.assert_array_equal(got, G[f"lr_{name}"])
+
+
+def test_lambda_lr_drives_param_groups():
+    p = torch.nn.Parameter(torch.zeros(4))
+    opt = torch.optim.SGD([p], lr=1.0)
+    sch = L.create_lr_scheduler(opt, "CONSTANT", warmup_steps=4, approximate_epoch_length=10, num_epochs=1)
+    lrs = []
+    for _ in range(6):
+        lrs.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sch.step()
+    assert lrs == [0.0, 0.25, 0.5, 0.75, 1.0, 1.0]
+
+
+def test_reference_presets_load():
+    ref = Path("/root/reference/training_presets")
+    if not ref.exists():
+        pytest.skip("reference presets not present on this host")
+    c = TrainConfig.load(str(ref / "#sdxl 1.0.json"))
+    assert c.model_type == "STABLE_DIFFUSION_XL_10_BASE" and c.weight_dtype == "BFLOAT_16"
+    assert c.vae.weight_dtype == "FLOAT_32" and c.text_encoder.train is False
+    c = TrainConfig.load(str(ref / "#sdxl 1.0 LoRA.json"))
+    assert c.training_method == "LORA"
+
+
+def test_flat_store_layout_and_fused_views():
+    st = FlatParamStore([("a", (3, 5), "g"), ("q", (8, 8), "g"), ("k", (8, 8), "g"), ("v", (8, 8), "g"),
+                         ("b", (7,), "h")], torch.bfloat16, "cpu")
+    for n, s in st.slots.items():
+        assert s.offset % 8 == 0
+    qkv = st.view(["q", "k", "v"], (24, 8))
+    qkv.fill_(2.0)
+    assert float(st.params["k"].sum()) == 128.0
+    assert st.params["q"].grad.data_ptr() == st.view(["q"], grad=True).data_ptr()
+    with pytest.raises(ValueError):
+        st.view(["a", "k"])
+    assert st.group_ranges()["h"][0] == st.slots["b"].offset
+
+
+def test_unet_specs_match_reference_sizes():
+    n_sdxl = sum(math.prod(s) for _, s, _, _ in U.unet_specs(U.sdxl_config()))
+    n_sd15 = sum(math.prod(s) for _, s, _, _ in U.unet_specs(U.sd15_config()))
+    assert n_sdxl == 2_567_463_684 and len(U.unet_specs(U.sdxl_config())) == 1680
+    assert n_sd15 == 859_520_964 and len(U.unet_specs(U.sd15_config())) == 686
+
+
+@pytest.mark.parametrize("cfgfn", [U.sdxl_config, U.sd15_config, U.tiny_sdxl_config])
+def test_unet_names_and_shapes_match_oracle(cfgfn):
+    cfg = cfgfn()
+    with torch.device("meta"):
+        om = OU.UNet2DConditionModel(OU.UNetConfig(**{k: getattr(cfg, k) for k in OU.UNetConfig.__dataclass_fields__}))
+    ours = {n: tuple(s) for n, s, _, _ in U.unet_specs(cfg)}
+    theirs = {n: tuple(p.shape) for n, p in om.named_parameters()}
+    assert ours == theirs
+
+
+def test_state_dict_roundtrip_cpu():
+    m = U.UNet2DConditionModel(U.tiny_sdxl_config(), "cpu", seed=3)
+    sd = m.state_dict()
+    m2 = U.UNet2DConditionModel(U.tiny_sdxl_config(), "cpu", seed=None)
+    m2.load_state_dict({k: v.float() for k, v in sd.items()})
+    assert torch.equal(m2.store.data, m.store.data)
+    assert torch.count_nonzero(m.store.params["conv_in.weight"][..., 4:]) == 0
+
+
+def test_flop_counter_matches_survey():
+    assert abs(U.flops_per_image(U.sdxl_config(), 128, 128) / 1e12 - 6.761) < 1e-3
+    assert abs(U.flops_per_image(U.sdxl_config(), 64, 64) / 1e12 - 1.589) < 1e-3
+    assert abs(U.flops_per_image(U.sd15_config(), 64, 64) / 1e12 - 0.803) < 1e-3
