@@ -67,6 +67,9 @@ typedef struct NormChunk { long long begin, end; int tensor, pad; } NormChunk;
 /* replaces: diffusers Linear/Conv2d fwd+bwd inside model.unet(...) (modules/modelSetup/BaseStableDiffusionXLSetup.py:268-273); conv/linear dgrad/wgrad of loss.backward() (modules/trainer/GenericTrainer.py:693-696) */
 int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_bytes, hipStream_t stream);
 
+/* plan query: workspace bytes otamd_gemm needs for `splits` (0 = automatic tile + split-K plan) */
+long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out);
+
 /* replaces: ABI check */
 int otamd_gemm_args_size(void);
 

@@ -62,6 +62,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_gemm_args_size": [],
     "otamd_conv_geom_size": [],
     "otamd_gemm": [C.POINTER(GemmArgs), I, VP, LL, VP],
+    "otamd_gemm_plan": [C.POINTER(GemmArgs), I, C.POINTER(C.c_int)],
     "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],
     "otamd_grad_clip_coef": [VP, I, VP, I, VP, I, F, VP, VP],
@@ -111,7 +112,7 @@ def lib():
         for name, args in SIGNATURES.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = C.c_longlong if name.endswith("_ws_floats") else C.c_int
+            fn.restype = C.c_longlong if (name.endswith("_ws_floats") or name.endswith("_plan")) else C.c_int
         _lib = L
     return _lib
 

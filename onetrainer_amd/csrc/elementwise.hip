@@ -144,13 +144,30 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16_t* __res
     ws[((long long)g * RB + rb) * N + c] = t;
   }
 }
-__global__ void colsum_reduce_kernel(const float* __restrict__ ws, int RB, int N, int groups, void* __restrict__ out,
-                                     int out_f32, int acc) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)groups * N;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long g = i / N, n = i - g * N;
+// second pass: block = 64 columns x 16 row-block lanes (float4 loads), grid = (N/64, groups)
+__global__ void __launch_bounds__(256) colsum_reduce_kernel(const float* __restrict__ ws, int RB, int N, int groups,
+                                                            void* __restrict__ out, int out_f32, int acc) {
+  __shared__ float red[16][64 + 4];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * 64 + cq * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < N) {
+    const float* p = ws + (long long)g * RB * N + c;
+#pragma unroll 4
+    for (int rb = rl; rb < RB; rb += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (long long)rb * N);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[rl][cq * 4 + 0] = s.x; red[rl][cq * 4 + 1] = s.y; red[rl][cq * 4 + 2] = s.z; red[rl][cq * 4 + 3] = s.w;
+  __syncthreads();
+  const int col = blockIdx.x * 64 + threadIdx.x;
+  if (threadIdx.x < 64 && col < N) {
     float t = 0.f;
-    for (int rb = 0; rb < RB; ++rb) t += ws[(g * RB + rb) * N + n];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+    const long long i = (long long)g * N + col;
     if (out_f32) {
       float* d = reinterpret_cast<float*>(out) + i;
       *d = acc ? *d + t : t;
@@ -267,7 +284,8 @@ OTAMD_API int otamd_upsample2x_bwd(const void* dup, void* dx, int N, int H, int 
 static int colsum_rpb(int rows_per_group, int N, int groups) {
   const int cblocks = (N + 255) / 256;
   int rpb = rows_per_group;
-  while (rpb > 64 && (long long)cblocks * groups * ((rows_per_group + rpb - 1) / rpb) < 1024) rpb = (rpb + 1) / 2;
+  // ~512 first-pass blocks; each then streams >= 64 rows (8 per thread-row) and RB stays small
+  while (rpb > 256 && (long long)cblocks * groups * ((rows_per_group + rpb - 1) / rpb) < 512) rpb = (rpb + 1) / 2;
   return rpb;
 }
 OTAMD_API long long otamd_colsum_ws_floats(int M, int N, int rows_per_group) {
@@ -285,7 +303,7 @@ OTAMD_API int otamd_colsum(const void* x, long long ldx, int M, int N, int rows_
   dim3 grid((N + 255) / 256, RB, groups);
   colsum_partial_kernel<<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, M, N, rows_per_group, rpb, RB, ws);
   OTAMD_CHECK_LAUNCH();
-  colsum_reduce_kernel<<<grid_for((long long)groups * N), 256, 0, s>>>(ws, RB, N, groups, out, out_f32, accumulate);
+  colsum_reduce_kernel<<<dim3((N + 63) / 64, groups), 256, 0, s>>>(ws, RB, N, groups, out, out_f32, accumulate);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

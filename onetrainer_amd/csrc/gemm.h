@@ -3,7 +3,9 @@
 #pragma once
 #include "common.h"
 
-enum { OPM_K = 0, OPM_MN = 1, OPM_CONV_FWD = 2, OPM_CONV_DGRAD = 3, OPM_CONV_WGRAD = 4 };
+// OPM_CONV_WT (v2 only): B of conv dgrad read straight from the stored weight W[Cout][KH][KW][Cin] as
+// an MN-mode operand B[k = tap*Cout + co][ci] (row address (co*KK + tap)*ld); gb.SC = Cout, gb.KH/KW.
+enum { OPM_K = 0, OPM_MN = 1, OPM_CONV_FWD = 2, OPM_CONV_DGRAD = 3, OPM_CONV_WGRAD = 4, OPM_CONV_WT = 5 };
 
 struct ConvGeom {
   int N;             // batch

@@ -7,7 +7,8 @@
 //   Linear dgrad dX = dY W          A: OPM_K (dY [M,N])    B: OPM_MN (W [N,K] read as [K'=N][N'=K])
 //   Linear wgrad dW = dY^T X        A: OPM_MN (dY)         B: OPM_MN (X)         (split-K slabs)
 //   conv fwd     implicit GEMM      A: OPM_CONV_FWD gather B: OPM_K (W [Cout][kh][kw][Cin])
-//   conv dgrad   transposed gather  A: OPM_CONV_DGRAD      B: OPM_K (W^T [Cin][kh][kw][Cout])
+//   conv dgrad   transposed gather  A: OPM_CONV_DGRAD      B: OPM_CONV_WT (W read in place, v2 tiles)
+//                                                          or OPM_K (W^T [Cin][kh][kw][Cout], any tile)
 //   conv wgrad   dW = dY^T im2col   A: OPM_MN (dY)         B: OPM_CONV_WGRAD gather
 // Activations are NHWC bf16, so a conv's rows are pixels and a Linear over tokens
 // reads the same tensor with no permute.
@@ -316,10 +317,13 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream);   // gemm2.hip
 
-// tile choice: -1 = v1 128x128 (4 waves), 0 = 256x256, 1 = 256x128, 2 = 128x256 (8 waves, LDS-DMA).
-// Cost model: waves of 256 CUs x tile work / relative per-CU throughput of the tile shape.
-// OTAMD_GEMM_TILE=v1|256x256|256x128|128x256 forces a choice (tests exercise every variant).
-static int choose_tile(int M, int N, int splits) {
+// Plan = (tile, splits).  tile: -1 = v1 128x128 (4 waves, 2 blocks/CU), 0 = 256x256, 1 = 256x128,
+// 2 = 128x256 (8 waves, 1 block/CU, LDS-DMA).  Cost model (seconds): waves of resident tiles x
+// (tile MACs / relative tile throughput + fixed prologue/epilogue) + split-K slab reduce traffic.
+// Relative throughputs are from tools/gemm_bench.py on MI355X.  OTAMD_GEMM_TILE forces the tile.
+struct GemmPlan { int tile, splits; };
+
+static int forced_tile() {
   static int forced = -2;
   if (forced == -2) {
     const char* e = getenv("OTAMD_GEMM_TILE");
@@ -331,16 +335,31 @@ static int choose_tile(int M, int N, int splits) {
       else if (!strcmp(e, "128x256")) forced = 2;
     }
   }
-  if (forced != -3) return forced;
-  const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256};
+  return forced;
+}
+
+static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = false) {
+  const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, per_cu[4] = {2, 1, 1, 1};
   const double rate[4] = {0.55, 1.0, 0.85, 0.85};
-  int best = -1;
-  double best_cost = 1e300;
+  const double cu_flops = 1.1e15 / 256.0;    // effective per-CU rate of the 256x256 tile
+  const int ft = forced_tile();
+  GemmPlan best = {-1, 1};
+  double best_t = 1e300;
   for (int t = 0; t < 4; ++t) {
-    const long long tiles = (long long)((M + bm[t] - 1) / bm[t]) * ((N + bn[t] - 1) / bn[t]) * splits;
-    const long long waves = (tiles + 255) / 256;
-    const double cost = (double)waves * bm[t] * bn[t] / rate[t];
-    if (cost < best_cost * 0.999) { best_cost = cost; best = t - 1; }
+    if (ft != -3 && t - 1 != ft) continue;
+    if (v2_only && t == 0) continue;
+    for (int s = 1; s <= max_splits; s *= 2) {
+      const long long kps = ((long long)(K + s - 1) / s + 63) / 64 * 64;
+      if (s > 1 && kps < 256) break;
+      const int se = (int)((K + kps - 1) / kps);
+      const long long tiles = (long long)((M + bm[t] - 1) / bm[t]) * ((N + bn[t] - 1) / bn[t]) * se;
+      const long long slots = 256LL * per_cu[t];
+      const long long waves = (tiles + slots - 1) / slots;
+      const double tile_t = 2.0 * bm[t] * bn[t] * (double)kps / (cu_flops * rate[t] / per_cu[t]);
+      double tt = waves * (tile_t + 2.5e-6);
+      if (se > 1) tt += ((double)se * M * N * 4.0 + (double)M * N * 2.0) / 4.5e12 + 3e-6;
+      if (tt < best_t * 0.98) { best_t = tt; best = {t - 1, se}; }
+    }
   }
   return best;
 }
@@ -349,13 +368,26 @@ static int choose_tile(int M, int N, int splits) {
 // operands need K % 8 == 0, MN-mode operands MN % 8 == 0; leading dims multiples of 8
 // elements; base pointers 16-byte aligned; conv gathers need SC % 8 == 0.
 // workspace: >= splits * M * N * 4 bytes when splits > 1.
+// workspace bytes otamd_gemm needs for `splits` (0 = automatic plan); *splits_out gets the plan's splits
+OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out) {
+  if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -1;
+  int s = splits;
+  if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT).splits;
+  if (splits_out) *splits_out = s;
+  return s > 1 ? (long long)s * in->M * in->N * 4 : 0;
+}
+
 OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_bytes, hipStream_t stream) {
   if (!in) return OTAMD_EINVAL;
   GemmArgs a = *in;
-  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 1) return OTAMD_EINVAL;
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
+  const bool v2_only = a.bmode == OPM_CONV_WT;
+  GemmPlan plan = plan_gemm(a.M, a.N, a.K, splits > 0 ? splits : 32, v2_only);
+  if (splits > 0) plan = plan_gemm(a.M, a.N, a.K, 1, v2_only), plan.splits = splits;
+  splits = plan.splits;
   if (!a.A || !a.B || !a.C || !aligned16(a.A) || !aligned16(a.B)) return OTAMD_EINVAL;
   gemm_fn fn = pick(a.amode, a.bmode);
-  if (!fn) return OTAMD_EUNSUPPORTED;
+  if (!fn && !v2_only) return OTAMD_EUNSUPPORTED;
   const bool ak = (a.amode != OPM_MN), bk = (a.bmode == OPM_K);
   if (ak && (a.K % 8)) return OTAMD_EINVAL;
   if (!ak && (a.M % 8)) return OTAMD_EINVAL;
@@ -374,11 +406,26 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
   } else {
     a.slab = nullptr;
   }
-  const int tile = choose_tile(a.M, a.N, splits);
+  int tile = plan.tile;
+  if (splits > 1 && forced_tile() == -3) {   // explicit splits: pick the best tile for them
+    tile = -1;
+    double bt = 1e300;
+    const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, pc[4] = {2, 1, 1, 1};
+    const double rate[4] = {0.55, 1.0, 0.85, 0.85};
+    for (int t = v2_only ? 1 : 0; t < 4; ++t) {
+      const long long tiles = (long long)((a.M + bm[t] - 1) / bm[t]) * ((a.N + bn[t] - 1) / bn[t]) * splits;
+      const double c = (double)((tiles + 256LL * pc[t] - 1) / (256LL * pc[t])) * bm[t] * bn[t] / rate[t] * pc[t];
+      if (c < bt * 0.98) { bt = c; tile = t - 1; }
+    }
+  } else if (forced_tile() != -3) {
+    tile = forced_tile();
+  }
+  if (v2_only && tile < 0) tile = 0;
   int rc = OTAMD_EUNSUPPORTED;
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
   if (rc != OTAMD_OK) {
+    if (!fn) return rc;
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid(tiles, 1, splits);
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);

@@ -34,6 +34,15 @@ __device__ __forceinline__ void wait_vmcnt() {
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
+// One 16-byte-per-lane LDS-DMA (1 KiB per wave). Issued as inline asm on purpose: the compiler's
+// waitcnt pass cannot prove that a later ds_read of the OTHER LDS stage does not alias an
+// in-flight builtin LDS-DMA and would drain vmcnt in front of it, serialising the pipeline.
+// Ordering is owned here: every read of a stage follows wait_vmcnt<> + BARRIER on its DMA.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned off) {
+  const unsigned m0 = (unsigned)(size_t)(lds_void_t*)lds;
+  asm volatile("buffer_load_dwordx4 %1, %2, 0 offen lds" ::"{m0}"(m0), "v"(off), "s"(rs) : "memory");
+}
+
 template <int MODE> struct IsKMode {
   static constexpr bool v = (MODE == OPM_K || MODE == OPM_CONV_FWD || MODE == OPM_CONV_DGRAD);
 };
@@ -75,7 +84,7 @@ struct Stage {
         const int col = mn0 + (lb * 2 + (pc & 1)) * 8;
         a[i] = r;
         ok[i] = col < MNsz;
-        if constexpr (MODE == OPM_MN) {
+        if constexpr (MODE == OPM_MN || MODE == OPM_CONV_WT) {
           b[i] = col;
         } else {   // OPM_CONV_WGRAD: col = (tap, ch)
           const int cc = ok[i] ? col : 0;
@@ -123,7 +132,7 @@ struct Stage {
           }
           if (v) off = (unsigned)(((a[i] * g.SH + sy) * g.SW + sx) * (int)g.ld + ch) * 2u;
         }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(img + (wave + 8 * i) * 1024), 16, (int)off, 0, 0, 0);
+        dma16(rs, img + (wave + 8 * i) * 1024, off);
       }
     } else {
 #pragma unroll
@@ -132,6 +141,11 @@ struct Stage {
         unsigned off = OFF_INVALID;
         if constexpr (MODE == OPM_MN) {
           if (ok[i] && k < Kend) off = (unsigned)(k * (int)ld + b[i]) * 2u;
+        } else if constexpr (MODE == OPM_CONV_WT) {   // k = tap*Cout + co -> W row co*KK + tap
+          if (ok[i] && k < Kend) {
+            const int tap = k / g.SC, co = k - tap * g.SC;
+            off = (unsigned)((co * (g.KH * g.KW) + tap) * (int)ld + b[i]) * 2u;
+          }
         } else {   // conv wgrad: k = output pixel
           bool v = ok[i] && k < Kend;
           const int kk = v ? k : 0;
@@ -145,7 +159,7 @@ struct Stage {
           else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
           if (v) off = (unsigned)(((n * g.SH + sy) * g.SW + sx) * (int)g.ld + c[i]) * 2u;
         }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(img + (wave + 8 * i) * 1024), 16, (int)off, 0, 0, 0);
+        dma16(rs, img + (wave + 8 * i) * 1024, off);
       }
     }
   }
@@ -210,54 +224,79 @@ __global__ void __launch_bounds__(512, 2) gemm2_kernel(GemmArgs args, unsigned a
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
+  // fragment loaders (h selects the 32-wide half of the 64-deep K tile)
+  auto load_a = [&](bf16x8 (&f)[MI], const char* ia, int h) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) f[i] = AK ? frag_k2(ia, wm * TM + i * 16, 32 * h) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 32 * h);
+  };
+  auto load_b = [&](bf16x8 (&f)[NJ], const char* ib, int h) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) f[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 32 * h) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 32 * h);
+  };
+  auto mfma_block = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+  };
+  // interleave the next fragment reads into the current MFMA block: {2 MFMA, reads of 1 fragment} x (MI+NJ)
+  auto interleave = [&]() {
+#pragma unroll
+    for (int t = 0; t < MI + NJ; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, AK && BKm ? 1 : 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ - 2 * (MI + NJ), 0);
+  };
+
+  // Pipeline, ONE barrier per K-step:
+  //   phase A: MFMA(h0 of tile k) || ds_read(h1 of tile k)
+  //   wait DMA(tile k+1); barrier  -- RAW for tile k+1, WAR for tile k's stage (all its reads retired)
+  //   DMA(tile k+2) -> stage of tile k
+  //   phase B: MFMA(h1 of tile k) || ds_read(h0 of tile k+1)
+  bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
   if (nk > 0) {
     sa.issue(ra, smem, args.ga, args.lda, kbeg, kend, wave);
     sb.issue(rb, smem + ABYTES, args.gb, args.ldb, kbeg, kend, wave);
-  }
-  if (nk > 1) {
-    sa.issue(ra, smem + STAGE, args.ga, args.lda, kbeg + 64, kend, wave);
-    sb.issue(rb, smem + STAGE + ABYTES, args.gb, args.ldb, kbeg + 64, kend, wave);
+    if (nk > 1) {
+      sa.issue(ra, smem + STAGE, args.ga, args.lda, kbeg + 64, kend, wave);
+      sb.issue(rb, smem + STAGE + ABYTES, args.gb, args.ldb, kbeg + 64, kend, wave);
+      wait_vmcnt<LOADS>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    BARRIER();
+    load_b(fb0, smem + ABYTES, 0);
+    load_a(fa0, smem, 0);
   }
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) wait_vmcnt<LOADS>(); else wait_vmcnt<0>();
-    BARRIER();
     const char* ia = smem + (kt & 1) * STAGE;
     const char* ib = ia + ABYTES;
-    // h = 0 fragments, then the h = 1 reads interleaved into the h = 0 MFMA block
-    // (<= 15 LDS reads outstanding so the compiler can count lgkmcnt), then the h = 1 block
-    bf16x8 af0[MI], bf0[NJ], af1[MI], bf1[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bf0[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 0) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 0);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) af0[i] = AK ? frag_k2(ia, wm * TM + i * 16, 0) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 0);
+    // phase A
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bf1[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 32) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 32);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) af1[i] = AK ? frag_k2(ia, wm * TM + i * 16, 32) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 32);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf0[j], af0[i], acc[i][j], 0, 0, 0);
-    // interleave: per step 1 LDS read group after every MFMA pair
-#pragma unroll
-    for (int t = 0; t < MI + NJ; ++t) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // 2 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, AK && BKm ? 1 : 2, 0);   // DS read(s) of one fragment
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ - 2 * (MI + NJ), 0);
+    load_b(fb1, ib, 1);
+    load_a(fa1, ia, 1);
+    mfma_block(fa0, fb0);
+    interleave();
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vmcnt<0>();       // tile k+1 (the only DMA in flight) has landed
     BARRIER();
     if (kt + 2 < nk) {
       char* nb = smem + (kt & 1) * STAGE;
       sa.issue(ra, nb, args.ga, args.lda, kbeg + (kt + 2) * 64, kend, wave);
       sb.issue(rb, nb + ABYTES, args.gb, args.ldb, kbeg + (kt + 2) * 64, kend, wave);
     }
+    // phase B
+    __builtin_amdgcn_sched_barrier(0);
+    {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
+      const char* na = smem + ((kt + 1) & 1) * STAGE;
+      load_b(fb0, na + ABYTES, 0);
+      load_a(fa0, na, 0);
+      mfma_block(fa1, fb1);
+      interleave();
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   const bool use_slab = gridDim.z > 1;
@@ -286,6 +325,7 @@ static gemm2_fn pick2(int am, int bm) {
   CASE2(OPM_MN, OPM_K)
   CASE2(OPM_CONV_FWD, OPM_K)
   CASE2(OPM_CONV_DGRAD, OPM_K)
+  CASE2(OPM_CONV_DGRAD, OPM_CONV_WT)
   CASE2(OPM_MN, OPM_CONV_WGRAD)
 #undef CASE2
   return nullptr;
@@ -295,7 +335,7 @@ static gemm2_fn pick2(int am, int bm) {
 static long long operand_bytes(int mode, const bf16_t* p, long long ld, int MN, int K, const ConvGeom& g) {
   (void)p;
   if (mode == OPM_K) return ((long long)(MN - 1) * ld + K) * 2;
-  if (mode == OPM_MN) return ((long long)(K - 1) * ld + MN) * 2;
+  if (mode == OPM_MN || mode == OPM_CONV_WT) return ((long long)(K - 1) * ld + MN) * 2;
   return ((long long)g.N * g.SH * g.SW - 1) * g.ld * 2 + (long long)g.SC * 2;
 }
 

@@ -17,7 +17,7 @@ from ._lib import ConvGeom, GemmArgs, check, lib
 BF16 = torch.bfloat16
 F32 = torch.float32
 
-OPM_K, OPM_MN, OPM_CONV_FWD, OPM_CONV_DGRAD, OPM_CONV_WGRAD = 0, 1, 2, 3, 4
+OPM_K, OPM_MN, OPM_CONV_FWD, OPM_CONV_DGRAD, OPM_CONV_WGRAD, OPM_CONV_WT = 0, 1, 2, 3, 4, 5
 
 
 def stream_handle() -> int:
@@ -48,9 +48,12 @@ def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 
 
 def _gemm(a: GemmArgs, splits: int, device) -> None:
-    ws_bytes = splits * a.M * a.N * 4 if splits > 1 else 0
-    ws = workspace(ws_bytes, device) if splits > 1 else None
-    check(lib().otamd_gemm(C.byref(a), splits, _p(ws), ws_bytes, stream_handle()), "otamd_gemm")
+    """splits = 0: the library plans tile shape and split-K (otamd_gemm_plan)."""
+    s_out = C.c_int(0)
+    ws_bytes = lib().otamd_gemm_plan(C.byref(a), splits, C.byref(s_out))
+    _req(ws_bytes >= 0, "gemm plan")
+    ws = workspace(ws_bytes, device) if ws_bytes > 0 else None
+    check(lib().otamd_gemm(C.byref(a), s_out.value, _p(ws), ws_bytes, stream_handle()), "otamd_gemm")
 
 
 def _new_args() -> GemmArgs:
@@ -117,7 +120,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, rowvec=No
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), out.stride(0) if M > 1 else N, int(out.dtype == F32), int(accumulate)
     a.M, a.N, a.K, a.alpha = M, N, K, alpha
     _epilogue(a, bias, rowvec, rows_per_vec, residual, M, N)
-    _gemm(a, 1, x.device)
+    _gemm(a, 0, x.device)
     return out
 
 
@@ -134,7 +137,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, acc
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), out.stride(0) if M > 1 else K, int(out.dtype == F32), int(accumulate)
     a.M, a.N, a.K = M, K, N
     _epilogue(a, None, None, 0, residual, M, K)
-    _gemm(a, 1, dy.device)
+    _gemm(a, 0, dy.device)
     return out
 
 
@@ -150,7 +153,7 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out=None, accumulate=False, 
     a.B, a.ldb, a.bmode = _p(x), _ld_rows(x), OPM_MN
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), out.stride(0), int(out.dtype == F32), int(accumulate)
     a.M, a.N, a.K = N, K, T
-    _gemm(a, splits or pick_splits(N, K, T), dy.device)
+    _gemm(a, splits or 0, dy.device)
     return out
 
 
@@ -199,16 +202,17 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, pad=1, upsampl
     a.M, a.N, a.K = M, Cout, KH * KW * Cin
     res2 = residual.reshape(M, Cout) if residual is not None else None
     _epilogue(a, bias, rowvec, P * Q if rowvec is not None else 0, res2, M, Cout)
-    _gemm(a, 1, x.device)
+    _gemm(a, 0, x.device)
     return out
 
 
-def conv2d_dgrad(dy: torch.Tensor, w_t: torch.Tensor, in_hw, stride=1, pad=1, out=None) -> torch.Tensor:
+def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw, stride=1, pad=1, out=None) -> torch.Tensor:
     """dx of conv2d (no upsample): dx[n,h,w,ci] = sum_{r,s,co} dy[n,(h+pad-r)/st,(w+pad-s)/st,co] * w[co,r,s,ci].
-    w_t is the weight transposed to [Cin][KH][KW][Cout] (conv_weight_transpose)."""
+    w is the stored weight [Cout][KH][KW][Cin], read in place (OPM_CONV_WT: no transpose pass)."""
     N, P, Q, Cout, ldy = _nhwc(dy)
-    Cin, KH, KW, Cout2 = w_t.shape
-    _req(Cout2 == Cout and w_t.is_contiguous() and Cin % 8 == 0, "w_t [Cin,KH,KW,Cout]")
+    Cout2, KH, KW, Cin = w.shape
+    _req(Cout2 == Cout and w.is_contiguous() and Cin % 8 == 0 and Cout % 8 == 0 and _aligned(w),
+         "w [Cout,KH,KW,Cin]")
     H, W = in_hw
     _req(conv_out_hw(H, W, KH, stride, pad) == (P, Q), "dgrad geometry")
     if out is None:
@@ -216,10 +220,11 @@ def conv2d_dgrad(dy: torch.Tensor, w_t: torch.Tensor, in_hw, stride=1, pad=1, ou
     a = _new_args()
     a.A, a.lda, a.amode = _p(dy), 8, OPM_CONV_DGRAD
     a.ga = _geom(N, P, Q, Cout, H, W, KH, KW, stride, pad, False, ldy)
-    a.B, a.ldb, a.bmode = _p(w_t), KH * KW * Cout, OPM_K
+    a.B, a.ldb, a.bmode = _p(w), Cin, OPM_CONV_WT
+    a.gb = _geom(N, P, Q, Cout, H, W, KH, KW, stride, pad, False, Cin)
     a.C, a.ldc = _p(out), Cin
     a.M, a.N, a.K = N * H * W, Cin, KH * KW * Cout
-    _gemm(a, 1, dy.device)
+    _gemm(a, 0, dy.device)
     return out
 
 
@@ -239,7 +244,7 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ksize=3, stride=1, pad=1, up
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), ksize * ksize * Cin, int(out.dtype == F32), int(accumulate)
     Kg = N * P * Q
     a.M, a.N, a.K = Cout, ksize * ksize * Cin, Kg
-    _gemm(a, splits or pick_splits(Cout, ksize * ksize * Cin, Kg), dy.device)
+    _gemm(a, splits or 0, dy.device)
     return out
 
 

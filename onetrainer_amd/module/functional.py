@@ -115,12 +115,11 @@ class ConvFn(torch.autograd.Function):
         N, H, W, _ = x.shape
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = K.conv_weight_transpose(wref.w)
             if ctx.upsample:
-                dup = K.conv2d_dgrad(dy, wt, (2 * H, 2 * W), 1, 1)
+                dup = K.conv2d_dgrad(dy, wref.w, (2 * H, 2 * W), 1, 1)
                 dx = K.upsample2x_bwd(dup)
             else:
-                dx = K.conv2d_dgrad(dy, wt, (H, W), ctx.stride, 1)
+                dx = K.conv2d_dgrad(dy, wref.w, (H, W), ctx.stride, 1)
         K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
         wref.done()
         drow = None

@@ -72,7 +72,8 @@ def to_nhwc(x):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,stride,up", [
     (2, 16, 16, 64, 128, 1, False), (2, 32, 24, 320, 320, 1, False), (1, 16, 16, 128, 64, 2, False),
-    (2, 8, 8, 128, 128, 1, True), (1, 64, 64, 8, 320, 1, False)])
+    (2, 8, 8, 128, 128, 1, True), (1, 64, 64, 8, 320, 1, False), (1, 16, 16, 320, 8, 1, False),
+    (2, 16, 8, 64, 72, 2, False)])
 def test_conv_fwd_dgrad_wgrad(dev, N, H, W, Cin, Cout, stride, up):
     torch.manual_seed(4)
     x = rnd(N, H, W, Cin, dev=dev)
@@ -88,7 +89,9 @@ def test_conv_fwd_dgrad_wgrad(dev, N, H, W, Cin, Cout, stride, up):
     ref.backward(nchw(dy))
     dw = K.conv2d_wgrad(dy, x, 3, stride, 1, upsample=up, out=torch.empty_like(w, dtype=torch.float32))
     close(dw, wr.grad.permute(0, 2, 3, 1), tol=1e-2)
-    if not up:
-        wt = w.permute(3, 1, 2, 0).contiguous()
-        dx = K.conv2d_dgrad(dy, wt, (H, W), stride, 1)
-        close(dx, to_nhwc(xr.grad))
+    # dgrad reads the stored [Cout][3][3][Cin] weight in place (B operand OPM_CONV_WT)
+    if up:
+        dx = K.upsample2x_bwd(K.conv2d_dgrad(dy, w, (2 * H, 2 * W), 1, 1))
+    else:
+        dx = K.conv2d_dgrad(dy, w, (H, W), stride, 1)
+    close(dx, to_nhwc(xr.grad))

@@ -59,11 +59,10 @@ for name, N, H, W, Ci, Co in CONVS:
     x = torch.randn(N, H, W, Ci, device=dev).to(BF)
     w = (torch.randn(Co, 3, 3, Ci, device=dev) * 0.02).to(BF)
     dy = torch.randn(N, H, W, Co, device=dev).to(BF)
-    wt = K.conv_weight_transpose(w)
     fl = 2.0 * N * H * W * Ci * Co * 9
     r = {"name": name, "shape": [N, H, W, Ci, Co]}
     r["fwd"] = fl / timeit(lambda: K.conv2d(x, w)) / 1e12
-    r["dgrad"] = fl / timeit(lambda: K.conv2d_dgrad(dy, wt, (H, W))) / 1e12
+    r["dgrad"] = fl / timeit(lambda: K.conv2d_dgrad(dy, w, (H, W))) / 1e12
     r["wgrad"] = fl / timeit(lambda: K.conv2d_wgrad(dy, x, out=torch.empty_like(w))) / 1e12
     xn = x.permute(0, 3, 1, 2)
     wn = w.permute(0, 3, 1, 2)
