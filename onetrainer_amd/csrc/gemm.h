@@ -32,6 +32,54 @@ struct GemmArgs {
 };
 
 
+__device__ __forceinline__ void add_bf8(float (&v)[8], const uint4& b) {
+  v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+  v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+  v[4] += __uint_as_float(b.z << 16); v[5] += __uint_as_float(b.z & 0xffff0000u);
+  v[6] += __uint_as_float(b.w << 16); v[7] += __uint_as_float(b.w & 0xffff0000u);
+}
+
+// true when every epilogue operand allows 16-byte accesses at 8-column granules (kernel-uniform)
+__device__ __forceinline__ bool gemm_wide_ok(const GemmArgs& a) {
+  const uintptr_t al = (uintptr_t)a.C | (uintptr_t)a.bias | (uintptr_t)a.rowvec | (uintptr_t)a.residual;
+  return (al & 15) == 0 && (a.ldc % 8) == 0 && (!a.rowvec || (a.ldv % 8) == 0) && (!a.residual || (a.ldr % 8) == 0);
+}
+
+// epilogue for 8 consecutive output columns n..n+7 of row m: same math as gemm_store4, 16-byte
+// loads / stores (half the store instructions of the 4-column form; the tail is issue-bound)
+__device__ __forceinline__ void gemm_store8(const GemmArgs& args, int m, int n, float (&v)[8], int split,
+                                            bool use_slab) {
+  if (use_slab) {
+    float* dst = args.slab + ((long long)split * args.M + m) * args.N + n;
+    reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) v[t] *= args.alpha;
+  if (args.bias) add_bf8(v, *reinterpret_cast<const uint4*>(args.bias + n));
+  if (args.rowvec) add_bf8(v, *reinterpret_cast<const uint4*>(args.rowvec + (long long)(m / args.rows_per_vec) * args.ldv + n));
+  if (args.residual) add_bf8(v, *reinterpret_cast<const uint4*>(args.residual + (long long)m * args.ldr + n));
+  if (args.c_f32) {
+    float4* dst = reinterpret_cast<float4*>(reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n);
+    if (args.accumulate) {
+      const float4 o0 = dst[0], o1 = dst[1];
+      v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w; v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+    }
+    dst[0] = make_float4(v[0], v[1], v[2], v[3]);
+    dst[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
+    if (args.accumulate) add_bf8(v, *reinterpret_cast<const uint4*>(dst));
+    uint4 o;
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(dst) = o;
+  }
+}
+
 // epilogue for 4 consecutive output columns n..n+3 of row m (fp32 accumulators in v[])
 __device__ __forceinline__ void gemm_store4(const GemmArgs& args, int m, int n, float (&v)[4], int split,
                                             bool use_slab) {
@@ -79,6 +127,19 @@ __device__ __forceinline__ void gemm_store4(const GemmArgs& args, int m, int n, 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// Grouped tile order: consecutive tile ids walk GM tile-rows down, then the next column, so the
+// ~32 tiles one XCD runs at a time (consecutive ids after xcd_remap) form an 8x4 block that shares
+// 8 A row-panels and 4 B column-panels in that XCD's L2 -- instead of one full column of A.
+__device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, int& tm, int& tn) {
+  constexpr int GM = 8;
+  const int per_group = GM * tiles_n;
+  const int g = wg / per_group, first = g * GM;
+  const int gsz = min(tiles_m - first, GM);
+  const int idx = wg - g * per_group;
+  tm = first + idx % gsz;
+  tn = idx / gsz;
 }
 
 // K-mode LDS image: [rows][64 k], 128-byte rows, 16-byte chunk c of row r stored at c ^ (r & 7)

@@ -194,7 +194,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs args) {
   const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tm = wg % tiles_m, tn = wg / tiles_m;
+  int tm, tn;
+  tile_coords(wg, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int split = blockIdx.z;
   const int kbeg = split * args.k_per_split;
@@ -333,6 +334,7 @@ static int forced_tile() {
       else if (!strcmp(e, "256x256")) forced = 0;
       else if (!strcmp(e, "256x128")) forced = 1;
       else if (!strcmp(e, "128x256")) forced = 2;
+      else if (!strcmp(e, "256x256w4")) forced = 3;
     }
   }
   return forced;

@@ -31,6 +31,8 @@ __device__ __forceinline__ void wait_vmcnt() {
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
@@ -47,11 +49,12 @@ template <int MODE> struct IsKMode {
   static constexpr bool v = (MODE == OPM_K || MODE == OPM_CONV_FWD || MODE == OPM_CONV_DGRAD);
 };
 
-// Per-lane DMA state of one operand tile (BMN rows/cols x 64 k), NI = BMN/64 pieces per lane.
-template <int MODE, int BMN>
+// Per-lane DMA state of one operand tile (BMN rows/cols x 64 k): BMN/8 pieces of 1 KiB, NW waves
+// take NI = BMN/(8 NW) each (piece j = wave + NW i).
+template <int MODE, int BMN, int NW>
 struct Stage {
   static constexpr bool KM = IsKMode<MODE>::v;
-  static constexpr int NI = BMN / 64;
+  static constexpr int NI = BMN / (8 * NW);
   static constexpr int RB = BMN * 2;      // MN-mode row bytes
   int a[NI], b[NI], c[NI];                // K: (row elem offset | conv n,y0,x0) ; MN: (k row, col, -)
   int t0, t1, t2;                         // K: logical chunk ; MN-conv: per-piece decode lives in a/b/c
@@ -60,7 +63,7 @@ struct Stage {
   __device__ __forceinline__ void prepare(const ConvGeom& g, long long ld, int mn0, int MNsz, int wave, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int j = wave + 8 * i;
+      const int j = wave + NW * i;
       if constexpr (KM) {
         const int r = 8 * j + (lane >> 3);
         const int gm = mn0 + r;
@@ -132,7 +135,7 @@ struct Stage {
           }
           if (v) off = (unsigned)(((a[i] * g.SH + sy) * g.SW + sx) * (int)g.ld + ch) * 2u;
         }
-        dma16(rs, img + (wave + 8 * i) * 1024, off);
+        dma16(rs, img + (wave + NW * i) * 1024, off);
       }
     } else {
 #pragma unroll
@@ -159,7 +162,7 @@ struct Stage {
           else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
           if (v) off = (unsigned)(((n * g.SH + sy) * g.SW + sx) * (int)g.ld + c[i]) * 2u;
         }
-        dma16(rs, img + (wave + 8 * i) * 1024, off);
+        dma16(rs, img + (wave + NW * i) * 1024, off);
       }
     }
   }
@@ -187,21 +190,25 @@ __device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int AM, int BMODE, int BM, int BN>
-__global__ void __launch_bounds__(512, 2) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes) {
+// NW = 8: 2 waves/SIMD (<= 256 VGPRs), wave tiles 128x64 / 64x64.  NW = 4: 1 wave/SIMD (512-entry
+// unified VGPR/AGPR file), 256x256 as 2x2 wave tiles of 128x128 -- a third less LDS read traffic
+// per MFMA (one 16x16x32 fragment read per 4 MFMAs instead of per 2.7).
+template <int AM, int BMODE, int BM, int BN, int NW>
+__global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int WN = (BM == 256 && BN == 128) ? 2 : 4;
-  constexpr int WM = 8 / WN;
+  constexpr int WN = NW == 4 ? 2 : ((BM == 256 && BN == 128) ? 2 : 4);
+  constexpr int WM = NW / WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MI = TM / 16, NJ = TN / 16;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
   constexpr int STAGE = ABYTES + BBYTES;
-  constexpr int LOADS = BM / 64 + BN / 64;
+  constexpr int LOADS = Stage<AM, BM, NW>::NI + Stage<BMODE, BN, NW>::NI;
   constexpr bool AK = IsKMode<AM>::v, BKm = IsKMode<BMODE>::v;
 
   const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = wg % tiles_m, tn = wg / tiles_m;
+  int tm, tn;
+  tile_coords(wg, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int split = blockIdx.z;
   const int kbeg = split * args.k_per_split;
@@ -212,8 +219,8 @@ __global__ void __launch_bounds__(512, 2) gemm2_kernel(GemmArgs args, unsigned a
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)args.A, (short)0, (int)a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)args.B, (short)0, (int)b_bytes, 0x00020000);
-  Stage<AM, BM> sa;
-  Stage<BMODE, BN> sb;
+  Stage<AM, BM, NW> sa;
+  Stage<BMODE, BN, NW> sb;
   sa.prepare(args.ga, args.lda, m0, args.M, wave, lane);
   sb.prepare(args.gb, args.ldb, n0, args.N, wave, lane);
 
@@ -300,13 +307,42 @@ __global__ void __launch_bounds__(512, 2) gemm2_kernel(GemmArgs args, unsigned a
   }
 
   const bool use_slab = gridDim.z > 1;
+  const int g = lane >> 4;
+  if (use_slab || gemm_wide_ok(args)) {
+    // Row blocks (i, i+1) of one column block exchange lane groups with v_permlane16_swap:
+    // afterwards lane group g holds 8 consecutive columns 8(g>>1).. of row block i + (g&1).
+#pragma unroll
+    for (int i = 0; i < MI; i += 2) {
+      const int m = m0 + wm * TM + (i + (g & 1)) * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][t]), __float_as_uint(acc[i + 1][j][t]),
+                                                          false, false);
+          v[t] = __uint_as_float(r[0]);
+          v[4 + t] = __uint_as_float(r[1]);
+        }
+        const int n = n0 + wn * TN + j * 16 + 8 * (g >> 1);
+        if (m >= args.M || n >= args.N) continue;
+        if (n + 8 <= args.N) {
+          gemm_store8(args, m, n, v, split, use_slab);
+        } else {
+          float v4[4] = {v[0], v[1], v[2], v[3]};
+          gemm_store4(args, m, n, v4, split, use_slab);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * TM + i * 16 + (lane & 15);
     if (m >= args.M) continue;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn * TN + j * 16 + 4 * (lane >> 4);
+      const int n = n0 + wn * TN + j * 16 + 4 * g;
       if (n >= args.N) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       gemm_store4(args, m, n, v, split, use_slab);
@@ -316,9 +352,9 @@ __global__ void __launch_bounds__(512, 2) gemm2_kernel(GemmArgs args, unsigned a
 
 typedef void (*gemm2_fn)(GemmArgs, unsigned, unsigned);
 
-template <int BM, int BN>
+template <int BM, int BN, int NW>
 static gemm2_fn pick2(int am, int bm) {
-#define CASE2(a, b) if (am == a && bm == b) return gemm2_kernel<a, b, BM, BN>;
+#define CASE2(a, b) if (am == a && bm == b) return gemm2_kernel<a, b, BM, BN, NW>;
   CASE2(OPM_K, OPM_K)
   CASE2(OPM_K, OPM_MN)
   CASE2(OPM_MN, OPM_MN)
@@ -346,17 +382,18 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   const long long bb = operand_bytes(a.bmode, a.B, a.ldb, a.N, a.K, a.gb);
   if (ab <= 0 || bb <= 0 || ab >= 0x7fff0000LL || bb >= 0x7fff0000LL) return OTAMD_EUNSUPPORTED;
   gemm2_fn fn = nullptr;
-  int BMv = 256, BNv = 256;
-  if (tile == 0) fn = pick2<256, 256>(a.amode, a.bmode);
-  else if (tile == 1) { fn = pick2<256, 128>(a.amode, a.bmode); BNv = 128; }
-  else { fn = pick2<128, 256>(a.amode, a.bmode); BMv = 128; }
+  int BMv = 256, BNv = 256, NWv = 8;
+  if (tile == 0) fn = pick2<256, 256, 8>(a.amode, a.bmode);
+  else if (tile == 1) { fn = pick2<256, 128, 8>(a.amode, a.bmode); BNv = 128; }
+  else if (tile == 2) { fn = pick2<128, 256, 8>(a.amode, a.bmode); BMv = 128; }
+  else { fn = pick2<256, 256, 4>(a.amode, a.bmode); NWv = 4; }
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
   const int lds = 2 * (BMv + BNv) * 128;
   static bool attr_set[3] = {false, false, false};
   (void)attr_set;
   hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(fn, dim3(tiles, 1, splits), dim3(512), lds, stream, a, (unsigned)ab, (unsigned)bb);
+  hipLaunchKernelGGL(fn, dim3(tiles, 1, splits), dim3(NWv * 64), lds, stream, a, (unsigned)ab, (unsigned)bb);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

@@ -38,13 +38,22 @@ def fma32(a, b, c) -> np.ndarray:
 
 
 def sr_bits(seed: int, idx: np.ndarray) -> np.ndarray:
-    """The HIP kernel's SR dither (onetrainer_amd/csrc/adamw.hip sr_bits): splitmix64 finalizer."""
+    """The HIP kernel's SR dither (onetrainer_amd/csrc/adamw.hip sr_bits): a 32-bit
+    multiply-xorshift hash of (element index, step seed); the dither is its high 16 bits.
+    (The reference draws torch.randint per step, bf16_stochastic_rounding.py:17-24; the
+    stream itself is not reproducible across implementations, only its distribution.)"""
+    U32 = np.uint32
+    idx = idx.astype(np.uint64)
+    k = U32((seed ^ (seed >> 32)) & 0xFFFFFFFF)
     with np.errstate(over="ignore"):
-        x = U64(seed) ^ (idx.astype(U64) * U64(0x9E3779B97F4A7C15))
-        x = (x ^ (x >> U64(30))) * U64(0xBF58476D1CE4E5B9)
-        x = (x ^ (x >> U64(27))) * U64(0x94D049BB133111EB)
-        x ^= x >> U64(31)
-    return (x & U64(0xFFFF)).astype(np.uint32)
+        x = (idx & np.uint64(0xFFFFFFFF)).astype(U32) * U32(0x9E3779B1) + k
+        x ^= (idx >> np.uint64(32)).astype(U32) * U32(0x85EBCA77)
+        x ^= x >> U32(16)
+        x *= U32(0x21F0AAAD)
+        x ^= x >> U32(15)
+        x *= U32(0x735A2D97)
+        x ^= x >> U32(15)
+    return (x >> U32(16)).astype(np.uint32)
 
 
 def copy_stochastic(source_f32: np.ndarray, rand16: np.ndarray) -> np.ndarray:

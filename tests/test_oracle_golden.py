@@ -94,7 +94,30 @@ def test_clip_grad_norm():
         assert np.array_equal(out[i], G[f"clip_out{i}"])
 
 
+def _sr_bits_py(seed, idx):
+    m = 0xFFFFFFFF
+    k = (seed ^ (seed >> 32)) & m
+    x = ((idx & m) * 0x9E3779B1 + k) & m
+    x ^= ((idx >> 32) * 0x85EBCA77) & m
+    x ^= x >> 16
+    x = (x * 0x21F0AAAD) & m
+    x ^= x >> 15
+    x = (x * 0x735A2D97) & m
+    x ^= x >> 15
+    return x >> 16
+
+
 def test_sr_bits_uniform():
     b = OA.sr_bits(42, np.arange(1 << 16))
     assert b.min() >= 0 and b.max() < (1 << 16)
     assert abs(b.mean() - 32767.5) < 300
+    bits = (b[:, None] >> np.arange(16)) & 1
+    assert np.all(np.abs(bits.mean(0) - 0.5) < 0.01)
+    # a different step seed gives an uncorrelated stream
+    b2 = OA.sr_bits(0x5851F42D4C957F2D, np.arange(1 << 16))
+    assert abs(np.corrcoef(b.astype(np.float64), b2.astype(np.float64))[0, 1]) < 0.02
+    # numpy restatement == scalar restatement, including indices past 2^32
+    idx = np.array([0, 1, 12345, (1 << 32) - 1, 1 << 32, (1 << 33) + 7], dtype=np.int64)
+    for seed in (0, 42, 0xFFFFFFFFFFFFFFFF):
+        got = OA.sr_bits(seed, idx)
+        assert [int(v) for v in got] == [_sr_bits_py(seed, int(i)) for i in idx]
