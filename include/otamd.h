@@ -82,6 +82,9 @@ int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream);
 /* replaces: autograd of scaled_dot_product_attention (GenericTrainer.py:693-696) */
 int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream);
 
+/* workspace bytes otamd_attn_bwd needs for these arguments ({lse, delta} pairs + split-query partials) */
+long long otamd_attn_bwd_ws_bytes(const AttnArgs* in);
+
 /* replaces: ABI check */
 int otamd_attn_args_size(void);
 

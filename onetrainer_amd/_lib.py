@@ -76,6 +76,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_attn_args_size": [],
     "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],
     "otamd_attn_bwd": [C.POINTER(AttnArgs), VP, LL, VP],
+    "otamd_attn_bwd_ws_bytes": [C.POINTER(AttnArgs)],
     # elementwise.hip
     "otamd_geglu_fwd": [VP, LL, VP, LL, I, I, VP],
     "otamd_geglu_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP],
@@ -112,7 +113,7 @@ def lib():
         for name, args in SIGNATURES.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = C.c_longlong if (name.endswith("_ws_floats") or name.endswith("_plan")) else C.c_int
+            fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_plan")) else C.c_int
         _lib = L
     return _lib
 

@@ -9,10 +9,17 @@
 //
 // Structure (per wave, 32 rows):
 //   forward / dQ : S^T = K Q^T  (keys in registers, query on the lane -> softmax row reduce is
-//                  lane-local + one xor-32 shuffle); P^T accumulator registers feed O^T = V^T P^T
+//                  lane-local + one permlane32 swap); P^T accumulator registers feed O^T = V^T P^T
 //                  directly as the MFMA B operand; V^T comes from ds_read_b64_tr_b16.
 //   dK/dV        : S = Q K^T with the key on the lane; P and dS accumulators feed
 //                  dV^T = dO^T P and dK^T = Q^T dS directly; dO^T, Q^T by transposed LDS reads.
+// Staging: every streamed tile (K/V for fwd and dQ, Q/dO and the {lse, delta} pairs for dK/dV)
+// goes HBM/L2 -> LDS by LDS-DMA (buffer_load ... lds) into an NS-deep ring, the swizzles applied
+// on the source address; one s_barrier per tile (RAW for tile t, WAR for the stage refilled
+// with tile t+NS-1).  Out-of-range rows / padded head columns are zero-filled by the
+// descriptor range check or an invalid offset.
+// Softmax VALU is kept under the MFMA time: packed fp32 math (v_pk_fma/mul), key masking only
+// on the partial last tile, and the forward's O rescale skipped when no lane's max grew.
 #include "common.h"
 
 struct AttnArgs {
@@ -28,17 +35,47 @@ struct AttnArgs {
 
 #define KT 64   // keys per staged tile (fwd / dQ)
 #define QT 32   // queries per staged tile (dK/dV)
+#define OFF_INVALID 0x80000000u
 static constexpr float LOG2E = 1.4426950408889634f;
 
 typedef __attribute__((address_space(3))) short4v lds_s4;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+#define MEMBAR() asm volatile("" ::: "memory")
+#define BARRIER()                 \
+  do {                            \
+    MEMBAR();                     \
+    __builtin_amdgcn_s_barrier(); \
+    MEMBAR();                     \
+  } while (0)
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// LDS-DMA, 16 / 4 bytes per lane (1 KiB / 256 B per wave instruction).  Inline asm so the
+// compiler's waitcnt pass does not drain vmcnt in front of ds_reads of other stages.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned off) {
+  const unsigned m0 = (unsigned)(size_t)(lds_void_t*)lds;
+  asm volatile("buffer_load_dwordx4 %1, %2, 0 offen lds" ::"{m0}"(m0), "v"(off), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned off) {
+  const unsigned m0 = (unsigned)(size_t)(lds_void_t*)lds;
+  asm volatile("buffer_load_dword %1, %2, 0 offen lds" ::"{m0}"(m0), "v"(off), "s"(rs) : "memory");
+}
+// make the compiler drain its own loads of x here (before any DMA it cannot see is in flight)
+template <typename T>
+__device__ __forceinline__ void consume(const T& x) { asm volatile("" ::"v"(x)); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
 
 // row image: [rows][D] bf16, 16-byte chunk c of row r stored at c ^ (r & 7)
-template <int D> __device__ __forceinline__ int row_off(int r, int c) { return r * (D * 2) + ((c ^ (r & 7)) << 4); }
 // transposed-read image: [rows][D] bf16, 32-byte block b of row r stored at b ^ sw(r)
+template <int D> __device__ __forceinline__ int tr_sw(int r) { return (D == 64) ? (((r >> 1) & 1) << 1) : ((r & 3) << 1); }
 template <int D> __device__ __forceinline__ int tr_off(int r, int col) {
-  const int blk = col >> 4, within = (col & 15) << 1;
-  const int sw = (D == 64) ? (((r >> 1) & 1) << 1) : ((r & 3) << 1);
-  return r * (D * 2) + ((blk ^ sw) << 5) + within;
+  return r * (D * 2) + (((col >> 4) ^ tr_sw<D>(r)) << 5) + ((col & 15) << 1);
 }
 
 __device__ __forceinline__ bf16x8 lds_row_frag(const char* img, int D2, int r, int c) {
@@ -78,36 +115,38 @@ __device__ __forceinline__ float16v zero16() {
 // row (in the 32-row accumulator tile) held by register i of this lane
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-// load a [rows x D] tile (token stride ld) into registers: NCH chunks per thread
-template <int D, int ROWS>
-struct TileLoader {
-  static constexpr int CH = D / 8;
-  static constexpr int NPER = ROWS * CH / 256;
-  bf8 v[NPER];
-  __device__ __forceinline__ void load(const bf16_t* base, long long ld, int row0, int nrows, int Dv) {
+// value of x in lane l ^ 32 (one permlane32 swap + select)
+__device__ __forceinline__ float xor32(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? s[0] : s[1]);
+}
+
+// DMA geometry of one [ROWS x D] bf16 image (row or transposed-read swizzle), split over 4 waves:
+// piece p (1 KiB) = wave + 4 i; lane l writes bytes [16 l, 16 l + 16) of the piece.
+template <int D, int ROWS, bool TR>
+struct DmaImg {
+  static constexpr int RB = D * 2;
+  static constexpr int NP = ROWS * RB / 1024;
+  static constexpr int PW = NP / 4;
+  static_assert(PW >= 1 && NP % 4 == 0, "image must split into whole pieces per wave");
+  int row[PW], col[PW];
+  __device__ __forceinline__ void prepare(int wave, int lane) {
 #pragma unroll
-    for (int i = 0; i < NPER; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / CH, c = idx % CH;
-      const bool ok = (row0 + r < nrows) && (c * 8 < Dv);
-      if (ok) v[i] = *reinterpret_cast<const bf8*>(base + (long long)(row0 + r) * ld + c * 8);
-      else { v[i].w[0] = v[i].w[1] = v[i].w[2] = v[i].w[3] = 0; }
+    for (int i = 0; i < PW; ++i) {
+      const int byte = (wave + 4 * i) * 1024 + lane * 16;
+      const int r = byte / RB, pos = (byte % RB) >> 4;
+      row[i] = r;
+      col[i] = TR ? ((((pos >> 1) ^ tr_sw<D>(r)) << 4) + ((pos & 1) << 3)) : ((pos ^ (r & 7)) << 3);
     }
   }
-  __device__ __forceinline__ void store_row(char* img) const {
+  // rows [row0, row0 + ROWS) of a [nrows x ld] operand whose descriptor starts at (batch, head)
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* img, long long ld, int row0, int nrows,
+                                        int Dv, int wave) const {
 #pragma unroll
-    for (int i = 0; i < NPER; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / CH, c = idx % CH;
-      *reinterpret_cast<bf8*>(img + row_off<D>(r, c)) = v[i];
-    }
-  }
-  __device__ __forceinline__ void store_tr(char* img) const {
-#pragma unroll
-    for (int i = 0; i < NPER; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / CH, c = idx % CH;
-      *reinterpret_cast<bf8*>(img + tr_off<D>(r, c * 8)) = v[i];
+    for (int i = 0; i < PW; ++i) {
+      const int rr = row0 + row[i];
+      const unsigned off = (rr < nrows && col[i] < Dv) ? (unsigned)(rr * (int)ld + col[i]) * 2u : OFF_INVALID;
+      dma16(rs, img + (wave + 4 * i) * 1024, off);
     }
   }
 };
@@ -125,20 +164,51 @@ __device__ __forceinline__ void load_row_frags(bf16x8 (&f)[D / 16], const bf16_t
   }
 }
 
+// P^T = exp2(S^T c - bias) in place, packed (v_pk_fma_f32 + v_exp_f32); masked keys already -inf
+__device__ __forceinline__ void exp2_scaled(float16v& S, float c, float bias) {
+  const f2v c2 = {c, c}, nb = {-bias, -bias};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    f2v x = {S[2 * k], S[2 * k + 1]};
+    x = x * c2 + nb;
+    S[2 * k] = __builtin_amdgcn_exp2f(x.x);
+    S[2 * k + 1] = __builtin_amdgcn_exp2f(x.y);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 template <int D>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TILE = KT * D * 2;   // bytes of one [64 x D] image
+  constexpr int TB = KT * D * 2;      // bytes of one [64 x D] image
+  constexpr int STG = 2 * TB;         // K row image + V transposed-read image
+  constexpr int NS = 3;
+  using KImg = DmaImg<D, KT, false>;
+  using VImg = DmaImg<D, KT, true>;
+  constexpr int LOADS = KImg::PW + VImg::PW;
   const int b = blockIdx.z, hh = blockIdx.y;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
   const int q0 = blockIdx.x * 128 + wave * 32;
   const bf16_t* Q = a.q + b * a.bsq + hh * a.Dv;
-  const bf16_t* Kp = a.k + b * a.bsk + hh * a.Dv;
-  const bf16_t* Vp = a.v + b * a.bsv + hh * a.Dv;
+  const auto rk = rsrc(a.k + b * a.bsk + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldk + a.Dv) * 2);
+  const auto rv = rsrc(a.v + b * a.bsv + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldv + a.Dv) * 2);
+  KImg ki;
+  VImg vi;
+  ki.prepare(wave, lane);
+  vi.prepare(wave, lane);
+  const int ntiles = (a.Nk + KT - 1) / KT;
 
   bf16x8 qf[D / 16];
   load_row_frags<D>(qf, Q, a.ldq, q0, a.Nq, a.Dv);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < ntiles) {
+      ki.issue(rk, smem + s * STG, a.ldk, s * KT, a.Nk, a.Dv, wave);
+      vi.issue(rv, smem + s * STG + TB, a.ldv, s * KT, a.Nk, a.Dv, wave);
+    }
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) consume(qf[s]);
   const float c = a.scale * LOG2E;
 
   float16v O[D / 32];
@@ -146,44 +216,56 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t) O[t] = zero16();
   float m = -INFINITY, l = 0.f;
 
-  TileLoader<D, KT> lk, lv;
-  const int ntiles = (a.Nk + KT - 1) / KT;
-  lk.load(Kp, a.ldk, 0, a.Nk, a.Dv);
-  lv.load(Vp, a.ldv, 0, a.Nk, a.Dv);
-  lk.store_row(smem);
-  lv.store_tr(smem + TILE);
-  __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    const char* kimg = smem + cur * 2 * TILE;
-    const char* vimg = kimg + TILE;
-    if (t + 1 < ntiles) { lk.load(Kp, a.ldk, (t + 1) * KT, a.Nk, a.Dv); lv.load(Vp, a.ldv, (t + 1) * KT, a.Nk, a.Dv); }
+    if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
+    else wait_vmcnt<0>();
+    BARRIER();
+    if (t + NS - 1 < ntiles) {
+      char* st = smem + ((t + NS - 1) % NS) * STG;
+      ki.issue(rk, st, a.ldk, (t + NS - 1) * KT, a.Nk, a.Dv, wave);
+      vi.issue(rv, st + TB, a.ldv, (t + NS - 1) * KT, a.Nk, a.Dv, wave);
+    }
+    const char* kimg = smem + (t % NS) * STG;
+    const char* vimg = kimg + TB;
 #pragma unroll
     for (int sub = 0; sub < KT / 32; ++sub) {
       float16v S = zero16();
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) S = mfma32(lds_row_frag(kimg, D * 2, sub * 32 + r, 2 * s + h), qf[s], S);
       const int kbase = t * KT + sub * 32;
-      float tmax = -INFINITY;
+      if (kbase + 32 > a.Nk) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float sv = (kbase + acc_row(i, h) < a.Nk) ? S[i] * c : -INFINITY;
-        S[i] = sv;
-        tmax = fmaxf(tmax, sv);
+        for (int i = 0; i < 16; ++i)
+          if (kbase + acc_row(i, h) >= a.Nk) S[i] = -INFINITY;
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m, tmax);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      float rs = 0.f;
+      float tmax = S[0];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { const float p = __builtin_amdgcn_exp2f(S[i] - mn); S[i] = p; rs += p; }
-      rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
-      m = mn;
+      for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, S[i]);
+      tmax = fmaxf(tmax, xor32(tmax));
+      const float mc = tmax * c;
+      if (__builtin_amdgcn_ballot_w64(mc > m) != 0) {   // wave-uniform: some row max grew
+        const float mn = fmaxf(m, mc);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        const f2v a2 = {alpha, alpha};
+        l *= alpha;
 #pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt)
+        for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) O[dt][i] *= alpha;
+          for (int k = 0; k < 8; ++k) {
+            f2v o = {O[dt][2 * k], O[dt][2 * k + 1]};
+            o *= a2;
+            O[dt][2 * k] = o.x;
+            O[dt][2 * k + 1] = o.y;
+          }
+        m = mn;
+      }
+      exp2_scaled(S, c, m);
+      f2v rs2 = {S[0], S[1]};
+#pragma unroll
+      for (int k = 1; k < 8; ++k) rs2 += f2v{S[2 * k], S[2 * k + 1]};
+      float rs = rs2.x + rs2.y;
+      rs += xor32(rs);
+      l += rs;
       const bf16x8 p0 = pack_acc(S, 0), p1 = pack_acc(S, 1);
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
@@ -191,12 +273,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         O[dt] = mfma32(tr_frag<D>(vimg, sub * 32, 1, dt * 32), p1, O[dt]);
       }
     }
-    if (t + 1 < ntiles) {
-      char* nimg = smem + (cur ^ 1) * 2 * TILE;
-      lk.store_row(nimg);
-      lv.store_tr(nimg + TILE);
-    }
-    __syncthreads();
   }
   const int q = q0 + r;
   if (q < a.Nq) {
@@ -218,8 +294,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   }
 }
 
-// delta[b,h,q] = sum_d dO * O  (fp32)
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, float* __restrict__ delta) {
+// pairs[b,h,q] = {lse2, delta}, delta = sum_d dO * O  (fp32)
+__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, float2* __restrict__ pairs) {
   const long long total = (long long)a.B * a.Nq * a.H;
   const int lane = threadIdx.x & 63;
   const int sub = lane & 7;    // 8 lanes per row, 8 elements each (Dv <= 64 per pass)
@@ -243,47 +319,69 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, float* 
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
-    if (sub == 0) delta[((long long)b * a.H + hh) * a.Nq + q] = s;
+    if (sub == 0) {
+      const long long i = ((long long)b * a.H + hh) * a.Nq + q;
+      pairs[i] = make_float2(a.lse[i], s);
+    }
   }
 }
 
-// dQ: per wave 32 queries, iterate over key tiles
+// dQ: per wave 32 queries, iterate over key tiles (K row + K transposed + V row images per stage)
 template <int D>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TILE = KT * D * 2;
+  constexpr int TB = KT * D * 2;
+  constexpr int STG = 3 * TB;
+  constexpr int NS = 3;
+  using RImg = DmaImg<D, KT, false>;
+  using TImg = DmaImg<D, KT, true>;
+  constexpr int LOADS = 2 * RImg::PW + TImg::PW;
   const int b = blockIdx.z, hh = blockIdx.y;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
   const int q0 = blockIdx.x * 128 + wave * 32;
-  const bf16_t* Kp = a.k + b * a.bsk + hh * a.Dv;
-  const bf16_t* Vp = a.v + b * a.bsv + hh * a.Dv;
+  const auto rk = rsrc(a.k + b * a.bsk + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldk + a.Dv) * 2);
+  const auto rv = rsrc(a.v + b * a.bsv + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldv + a.Dv) * 2);
+  RImg ri;
+  TImg ti;
+  ri.prepare(wave, lane);
+  ti.prepare(wave, lane);
+  const int ntiles = (a.Nk + KT - 1) / KT;
+  auto issue = [&](int t, char* st) {
+    ri.issue(rk, st, a.ldk, t * KT, a.Nk, a.Dv, wave);
+    ti.issue(rk, st + TB, a.ldk, t * KT, a.Nk, a.Dv, wave);
+    ri.issue(rv, st + 2 * TB, a.ldv, t * KT, a.Nk, a.Dv, wave);
+  };
+
   bf16x8 qf[D / 16], gf[D / 16];
   load_row_frags<D>(qf, a.q + b * a.bsq + hh * a.Dv, a.ldq, q0, a.Nq, a.Dv);
   load_row_frags<D>(gf, a.dout + b * a.bsdo + hh * a.Dv, a.lddo, q0, a.Nq, a.Dv);
-  const float c = a.scale * LOG2E;
   const int q = q0 + r;
   const long long srow = ((long long)b * a.H + hh) * a.Nq;
-  const float lse2 = q < a.Nq ? a.lse[srow + q] : 0.f;
-  const float dlt = q < a.Nq ? a.delta[srow + q] : 0.f;
+  const float2 pr = q < a.Nq ? reinterpret_cast<const float2*>(a.delta)[srow + q] : make_float2(0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < ntiles) issue(s, smem + s * STG);
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) { consume(qf[s]); consume(gf[s]); }
+  consume(pr.x);
+  consume(pr.y);
+  const float lse2 = pr.x, dlt = pr.y;
+  const float c = a.scale * LOG2E;
+  const f2v dl2 = {dlt, dlt};
 
   float16v dQ[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dQ[t] = zero16();
 
-  TileLoader<D, KT> lk, lv;
-  const int ntiles = (a.Nk + KT - 1) / KT;
-  lk.load(Kp, a.ldk, 0, a.Nk, a.Dv);
-  lv.load(Vp, a.ldv, 0, a.Nk, a.Dv);
-  lk.store_row(smem);
-  lk.store_tr(smem + TILE);
-  lv.store_row(smem + 2 * TILE);
-  __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    const char* krow = smem + cur * 3 * TILE;
-    const char* ktr = krow + TILE;
-    const char* vrow = krow + 2 * TILE;
-    if (t + 1 < ntiles) { lk.load(Kp, a.ldk, (t + 1) * KT, a.Nk, a.Dv); lv.load(Vp, a.ldv, (t + 1) * KT, a.Nk, a.Dv); }
+    if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
+    else wait_vmcnt<0>();
+    BARRIER();
+    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((t + NS - 1) % NS) * STG);
+    const char* krow = smem + (t % NS) * STG;
+    const char* ktr = krow + TB;
+    const char* vrow = krow + 2 * TB;
 #pragma unroll
     for (int sub = 0; sub < KT / 32; ++sub) {
       float16v S = zero16(), dP = zero16();
@@ -293,11 +391,18 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
         dP = mfma32(lds_row_frag(vrow, D * 2, sub * 32 + r, 2 * s + h), gf[s], dP);
       }
       const int kbase = t * KT + sub * 32;
+      if (kbase + 32 > a.Nk) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const bool ok = kbase + acc_row(i, h) < a.Nk;
-        const float p = ok ? __builtin_amdgcn_exp2f(S[i] * c - lse2) : 0.f;
-        S[i] = p * (dP[i] - dlt);   // dS^T
+        for (int i = 0; i < 16; ++i)
+          if (kbase + acc_row(i, h) >= a.Nk) S[i] = -INFINITY;
+      }
+      exp2_scaled(S, c, lse2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {   // dS^T = P^T (dP^T - delta)
+        f2v p = {S[2 * k], S[2 * k + 1]}, d = {dP[2 * k], dP[2 * k + 1]};
+        p = p * (d - dl2);
+        S[2 * k] = p.x;
+        S[2 * k + 1] = p.y;
       }
       const bf16x8 s0 = pack_acc(S, 0), s1 = pack_acc(S, 1);
 #pragma unroll
@@ -306,13 +411,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
         dQ[dt] = mfma32(tr_frag<D>(ktr, sub * 32, 1, dt * 32), s1, dQ[dt]);
       }
     }
-    if (t + 1 < ntiles) {
-      char* nimg = smem + (cur ^ 1) * 3 * TILE;
-      lk.store_row(nimg);
-      lk.store_tr(nimg + TILE);
-      lv.store_row(nimg + 2 * TILE);
-    }
-    __syncthreads();
   }
   if (q < a.Nq) {
     bf16_t* Dp = a.dq + b * a.bsdq + (long long)q * a.lddq + hh * a.Dv;
@@ -331,70 +429,74 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
-// dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of 32 in this split's range
+// dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of 32 in this split's range.
+// Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 {lse, delta} pairs.
 template <int D>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TILE = QT * D * 2;                 // one [32 x D] image
-  constexpr int STAGE = 4 * TILE + 2 * QT * 4;     // q row, q tr, do row, do tr, lse2, delta
+  constexpr int TB = QT * D * 2;                 // one [32 x D] image
+  constexpr int STG = 4 * TB + QT * 8;           // + 32 float2 pairs
+  constexpr int NS = 3;                          // 50 KiB (D = 64): 3 blocks per CU
+  using RImg = DmaImg<D, QT, false>;
+  using TImg = DmaImg<D, QT, true>;
+  constexpr int LOADS = 2 * RImg::PW + 2 * TImg::PW + 1;
   const int bz = blockIdx.z;
   const int b = bz / a.qsplit, split = bz % a.qsplit;
   const int hh = blockIdx.y;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
   const int k0 = blockIdx.x * 128 + wave * 32;
-  bf16x8 kf[D / 16], vf[D / 16];
-  load_row_frags<D>(kf, a.k + b * a.bsk + hh * a.Dv, a.ldk, k0, a.Nk, a.Dv);
-  load_row_frags<D>(vf, a.v + b * a.bsv + hh * a.Dv, a.ldv, k0, a.Nk, a.Dv);
-  const float c = a.scale * LOG2E;
-  const bf16_t* Qp = a.q + b * a.bsq + hh * a.Dv;
-  const bf16_t* Gp = a.dout + b * a.bsdo + hh * a.Dv;
   const long long srow = ((long long)b * a.H + hh) * a.Nq;
+  const auto rq = rsrc(a.q + b * a.bsq + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldq + a.Dv) * 2);
+  const auto rg = rsrc(a.dout + b * a.bsdo + hh * a.Dv, ((long long)(a.Nq - 1) * a.lddo + a.Dv) * 2);
+  const auto rp = rsrc(a.delta + 2 * srow, (long long)a.Nq * 8);
+  RImg ri;
+  TImg ti;
+  ri.prepare(wave, lane);
+  ti.prepare(wave, lane);
 
   const int per = (((a.Nq + a.qsplit - 1) / a.qsplit) + QT - 1) / QT * QT;
   const int qbeg = split * per;
   const int qend = min(a.Nq, qbeg + per);
   const int ntiles = qend > qbeg ? (qend - qbeg + QT - 1) / QT : 0;
+  auto issue = [&](int t, char* st) {
+    const int qt0 = qbeg + t * QT;
+    ri.issue(rq, st, a.ldq, qt0, qend, a.Dv, wave);
+    ti.issue(rq, st + TB, a.ldq, qt0, qend, a.Dv, wave);
+    ri.issue(rg, st + 2 * TB, a.lddo, qt0, qend, a.Dv, wave);
+    ti.issue(rg, st + 3 * TB, a.lddo, qt0, qend, a.Dv, wave);
+    if ((lane >> 4) == wave) {   // 64 floats = 32 pairs; wave w moves floats 16w .. 16w+15
+      const unsigned off = (qt0 + (lane >> 1) < qend) ? (unsigned)(2 * qt0 + lane) * 4u : OFF_INVALID;
+      dma4(rp, st + 4 * TB, off);
+    }
+  };
+
+  bf16x8 kf[D / 16], vf[D / 16];
+  load_row_frags<D>(kf, a.k + b * a.bsk + hh * a.Dv, a.ldk, k0, a.Nk, a.Dv);
+  load_row_frags<D>(vf, a.v + b * a.bsv + hh * a.Dv, a.ldv, k0, a.Nk, a.Dv);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < ntiles) issue(s, smem + s * STG);
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) { consume(kf[s]); consume(vf[s]); }
+  const float c = a.scale * LOG2E;
+  const f2v c2 = {c, c};
 
   float16v dK[D / 32], dV[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) { dK[t] = zero16(); dV[t] = zero16(); }
 
-  TileLoader<D, QT> lq, lg;
-  float ls_v = 0.f, dl_v = 0.f;   // thread t < 32 stages lse2/delta of query t
-  auto load_stage = [&](int qt0) {
-    lq.load(Qp, a.ldq, qt0, qend, a.Dv);
-    lg.load(Gp, a.lddo, qt0, qend, a.Dv);
-    if (threadIdx.x < QT) {
-      const int qq = qt0 + threadIdx.x;
-      ls_v = qq < qend ? a.lse[srow + qq] : INFINITY;
-      dl_v = qq < qend ? a.delta[srow + qq] : 0.f;
-    }
-  };
-  auto store_stage = [&](char* st) {
-    lq.store_row(st);
-    lq.store_tr(st + TILE);
-    lg.store_row(st + 2 * TILE);
-    lg.store_tr(st + 3 * TILE);
-    if (threadIdx.x < QT) {
-      reinterpret_cast<float*>(st + 4 * TILE)[threadIdx.x] = ls_v;
-      reinterpret_cast<float*>(st + 4 * TILE)[QT + threadIdx.x] = dl_v;
-    }
-  };
-  if (ntiles > 0) {
-    load_stage(qbeg);
-    store_stage(smem);
-    __syncthreads();
-  }
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    const char* st = smem + cur * STAGE;
+    if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
+    else wait_vmcnt<0>();
+    BARRIER();
+    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((t + NS - 1) % NS) * STG);
+    const char* st = smem + (t % NS) * STG;
     const char* qrow = st;
-    const char* qtr = st + TILE;
-    const char* grow = st + 2 * TILE;
-    const char* gtr = st + 3 * TILE;
-    const float* lsv = reinterpret_cast<const float*>(st + 4 * TILE);
-    const float* dlv = lsv + QT;
-    if (t + 1 < ntiles) load_stage(qbeg + (t + 1) * QT);
+    const char* qtr = st + TB;
+    const char* grow = st + 2 * TB;
+    const char* gtr = st + 3 * TB;
+    const float4* pv = reinterpret_cast<const float4*>(st + 4 * TB);   // pv[j] = pairs 2j, 2j+1
     float16v S = zero16(), dP = zero16();
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
@@ -402,11 +504,23 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(AttnArgs a) {
       dP = mfma32(lds_row_frag(grow, D * 2, r, 2 * s + h), vf[s], dP);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qr = acc_row(i, h);
-      const float p = __builtin_amdgcn_exp2f(S[i] * c - lsv[qr]);
-      S[i] = p;
-      dP[i] = p * (dP[i] - dlv[qr]);
+    for (int g = 0; g < 4; ++g) {      // registers 4g..4g+3 <-> queries 8g + 4h + (0..3)
+      const int q4 = 8 * g + 4 * h;
+      const float4 p01 = pv[q4 >> 1], p23 = pv[(q4 >> 1) + 1];   // {lse,dl} of q4, q4+1 | q4+2, q4+3
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float4 pp = e ? p23 : p01;
+        f2v x = {S[4 * g + 2 * e], S[4 * g + 2 * e + 1]};
+        const f2v ls = {pp.x, pp.z}, dl = {pp.y, pp.w};
+        x = x * c2 - ls;
+        f2v p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+        f2v d = {dP[4 * g + 2 * e], dP[4 * g + 2 * e + 1]};
+        d = p * (d - dl);
+        S[4 * g + 2 * e] = p.x;
+        S[4 * g + 2 * e + 1] = p.y;
+        dP[4 * g + 2 * e] = d.x;
+        dP[4 * g + 2 * e + 1] = d.y;
+      }
     }
     const bf16x8 p0 = pack_acc(S, 0), p1 = pack_acc(S, 1);
     const bf16x8 s0 = pack_acc(dP, 0), s1 = pack_acc(dP, 1);
@@ -417,8 +531,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(AttnArgs a) {
       dK[dt] = mfma32(tr_frag<D>(qtr, 0, 0, dt * 32), s0, dK[dt]);
       dK[dt] = mfma32(tr_frag<D>(qtr, 0, 1, dt * 32), s1, dK[dt]);
     }
-    if (t + 1 < ntiles) store_stage(smem + (cur ^ 1) * STAGE);
-    __syncthreads();
   }
   const int key = k0 + r;
   if (key < a.Nk) {
@@ -428,14 +540,13 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(AttnArgs a) {
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * h;
         if (d >= a.Dv) continue;
-        if (a.qsplit > 1) {
-          float* kp = a.dk32 + (((long long)b * a.Nk + key) * a.H + hh) * a.Dv + d;
-          float* vp = a.dv32 + (((long long)b * a.Nk + key) * a.H + hh) * a.Dv + d;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            atomicAdd(kp + e, dK[dt][4 * g + e] * a.scale);
-            atomicAdd(vp + e, dV[dt][4 * g + e]);
-          }
+        if (a.qsplit > 1) {   // this split's fp32 slab [qsplit][B][Nk][H][Dv]; summed by attn_dkv_cast
+          const long long base = ((((long long)split * a.B + b) * a.Nk + key) * a.H + hh) * a.Dv + d;
+          *reinterpret_cast<float4*>(a.dk32 + base) =
+              make_float4(dK[dt][4 * g] * a.scale, dK[dt][4 * g + 1] * a.scale, dK[dt][4 * g + 2] * a.scale,
+                          dK[dt][4 * g + 3] * a.scale);
+          *reinterpret_cast<float4*>(a.dv32 + base) =
+              make_float4(dV[dt][4 * g], dV[dt][4 * g + 1], dV[dt][4 * g + 2], dV[dt][4 * g + 3]);
         } else {
           bf16_t* kp = a.dk + b * a.bsdk + (long long)key * a.lddk + hh * a.Dv + d;
           bf16_t* vp = a.dv + b * a.bsdv + (long long)key * a.lddv + hh * a.Dv + d;
@@ -451,26 +562,51 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
-// fp32 [B, Nk, H, Dv] partials -> bf16 dK / dV with their strides
+// sum the qsplit fp32 slabs [qsplit][B, Nk, H, Dv] -> bf16 dK / dV with their strides (4 elements
+// per thread; Dv % 8 == 0).  Deterministic: fixed summation order over the splits.
 __global__ void attn_dkv_cast_kernel(AttnArgs a) {
-  const long long total = (long long)a.B * a.Nk * a.H * a.Dv;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+  const long long total4 = (long long)a.B * a.Nk * a.H * a.Dv / 4;
+  const long long slab = total4 * 4;
+  for (long long i4 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i4 < total4; i4 += (long long)gridDim.x * blockDim.x) {
+    const long long i = i4 * 4;
+    float4 sk = *reinterpret_cast<const float4*>(a.dk32 + i), sv = *reinterpret_cast<const float4*>(a.dv32 + i);
+    for (int s = 1; s < a.qsplit; ++s) {
+      const float4 k = *reinterpret_cast<const float4*>(a.dk32 + s * slab + i);
+      const float4 v = *reinterpret_cast<const float4*>(a.dv32 + s * slab + i);
+      sk.x += k.x; sk.y += k.y; sk.z += k.z; sk.w += k.w;
+      sv.x += v.x; sv.y += v.y; sv.z += v.z; sv.w += v.w;
+    }
     const int d = (int)(i % a.Dv);
     long long t = i / a.Dv;
     const int hh = (int)(t % a.H);
     t /= a.H;
     const int key = (int)(t % a.Nk), b = (int)(t / a.Nk);
-    a.dk[b * a.bsdk + (long long)key * a.lddk + hh * a.Dv + d] = f2bf(a.dk32[i]);
-    a.dv[b * a.bsdv + (long long)key * a.lddv + hh * a.Dv + d] = f2bf(a.dv32[i]);
+    uint2 wk, wv;
+    wk.x = (uint32_t)f2bf(sk.x) | ((uint32_t)f2bf(sk.y) << 16);
+    wk.y = (uint32_t)f2bf(sk.z) | ((uint32_t)f2bf(sk.w) << 16);
+    wv.x = (uint32_t)f2bf(sv.x) | ((uint32_t)f2bf(sv.y) << 16);
+    wv.y = (uint32_t)f2bf(sv.z) | ((uint32_t)f2bf(sv.w) << 16);
+    *reinterpret_cast<uint2*>(a.dk + b * a.bsdk + (long long)key * a.lddk + hh * a.Dv + d) = wk;
+    *reinterpret_cast<uint2*>(a.dv + b * a.bsdv + (long long)key * a.lddv + hh * a.Dv + d) = wv;
   }
 }
+
+// the per-(batch, head) DMA descriptors address rows with 31-bit byte offsets
+static bool fits31(int rows, long long ld) { return ((long long)rows * ld + 128) * 2 < 0x7fff0000LL; }
 
 static bool attn_ok(const AttnArgs& a) {
   if (a.B <= 0 || a.H <= 0 || a.Nq <= 0 || a.Nk <= 0 || a.Dv <= 0 || a.Dv % 8 || a.Dv > 128) return false;
   const long long lds[] = {a.ldq, a.ldk, a.ldv, a.bsq, a.bsk, a.bsv};
   for (long long v : lds) if (v % 8) return false;
   if (((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v) & 15) return false;
+  if (!fits31(a.Nq, a.ldq) || !fits31(a.Nk, a.ldk) || !fits31(a.Nk, a.ldv)) return false;
   return true;
+}
+
+template <typename K>
+static void launch(K kern, dim3 grid, int lds, hipStream_t s, const AttnArgs& a) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
 }
 
 OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
@@ -478,51 +614,64 @@ OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
   AttnArgs a = *in;
   if (a.ldo % 4 || a.bso % 4) return OTAMD_EINVAL;
   dim3 grid((a.Nq + 127) / 128, a.H, a.B);
-  if (a.Dv <= 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 2 * 2 * KT * 64 * 2, stream, a);
-  else hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 2 * 2 * KT * 128 * 2, stream, a);
+  if (a.Dv <= 64) launch(attn_fwd_kernel<64>, grid, 3 * 2 * KT * 64 * 2, stream, a);
+  else launch(attn_fwd_kernel<128>, grid, 3 * 2 * KT * 128 * 2, stream, a);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
 
-// ws: float[B*H*Nq] for delta + (qsplit>1 ? 2*B*Nk*H*Dv floats) ; lse from the forward
-OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream) {
-  if (!in || !attn_ok(*in) || !in->o || !in->lse || !in->dout || !in->dq || !in->dk || !in->dv || !ws) return OTAMD_EINVAL;
-  AttnArgs a = *in;
-  if (a.lddo % 8 || a.bsdo % 8 || a.lddq % 4 || a.lddk % 4 || a.lddv % 4) return OTAMD_EINVAL;
-  const long long nrow = (long long)a.B * a.H * a.Nq;
-  const long long nkv = (long long)a.B * a.Nk * a.H * a.Dv;
-  // parallelism for dK/dV: split the query range when there are few key blocks
+static int attn_qsplit(const AttnArgs& a) {
   const int kblocks = (a.Nk + 127) / 128;
   int qsplit = 1;
   while (kblocks * a.H * a.B * qsplit < 512 && qsplit < 64 && (a.Nq / (qsplit * 2)) >= 128) qsplit *= 2;
+  return qsplit;
+}
+
+// workspace bytes otamd_attn_bwd needs: {lse, delta} pairs + (split queries) fp32 dK/dV partials
+OTAMD_API long long otamd_attn_bwd_ws_bytes(const AttnArgs* in) {
+  if (!in || in->B <= 0 || in->H <= 0 || in->Nq <= 0 || in->Nk <= 0 || in->Dv <= 0) return -1;
+  const long long nrow = (long long)in->B * in->H * in->Nq;
+  const long long nkv = (long long)in->B * in->Nk * in->H * in->Dv;
+  const int qs = attn_qsplit(*in);
+  return nrow * 8 + 256 + (qs > 1 ? 2LL * qs * nkv * 4 : 0);
+}
+
+// ws: otamd_attn_bwd_ws_bytes(args) bytes, 16-byte aligned; lse from the forward
+OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream) {
+  if (!in || !attn_ok(*in) || !in->o || !in->lse || !in->dout || !in->dq || !in->dk || !in->dv || !ws) return OTAMD_EINVAL;
+  AttnArgs a = *in;
+  if (a.lddo % 8 || a.bsdo % 8 || a.lddq % 4 || a.lddk % 4 || a.lddv % 4 || ((uintptr_t)ws & 15)) return OTAMD_EINVAL;
+  if (((uintptr_t)a.dout & 15) || !fits31(a.Nq, a.lddo)) return OTAMD_EINVAL;
+  const long long nrow = (long long)a.B * a.H * a.Nq;
+  const long long nkv = (long long)a.B * a.Nk * a.H * a.Dv;
+  const int qsplit = attn_qsplit(a);
   a.qsplit = qsplit;
-  const long long need = nrow * 4 + (qsplit > 1 ? 2 * nkv * 4 : 0);
-  if (ws_bytes < need) return OTAMD_EINVAL;
-  float* delta = ws;
-  a.delta = delta;
-  if (qsplit > 1) {
-    a.dk32 = ws + ((nrow + 3) / 4) * 4;
-    a.dv32 = a.dk32 + nkv;
-    if (hipMemsetAsync(a.dk32, 0, 2 * nkv * 4, stream) != hipSuccess) return OTAMD_ELAUNCH;
+  if (ws_bytes < otamd_attn_bwd_ws_bytes(in)) return OTAMD_EINVAL;
+  float2* pairs = reinterpret_cast<float2*>(ws);
+  a.delta = ws;
+  if (qsplit > 1) {   // every slab element is written by exactly one block: no memset
+    a.dk32 = ws + ((nrow * 2 + 64) / 64) * 64;
+    a.dv32 = a.dk32 + (long long)qsplit * nkv;
   }
   {
     long long threads = nrow * 8;
     int blocks = (int)std::min<long long>((threads + 255) / 256, 8192);
-    attn_bwd_delta_kernel<<<blocks, 256, 0, stream>>>(a, delta);
+    attn_bwd_delta_kernel<<<blocks, 256, 0, stream>>>(a, pairs);
     OTAMD_CHECK_LAUNCH();
   }
+  const int kblocks = (a.Nk + 127) / 128;
   dim3 gq((a.Nq + 127) / 128, a.H, a.B);
   dim3 gk(kblocks, a.H, a.B * qsplit);
   if (a.Dv <= 64) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, gq, dim3(256), 2 * 3 * KT * 64 * 2, stream, a);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, gk, dim3(256), 2 * (4 * QT * 64 * 2 + 2 * QT * 4), stream, a);
+    launch(attn_bwd_dq_kernel<64>, gq, 3 * 3 * KT * 64 * 2, stream, a);
+    launch(attn_bwd_dkv_kernel<64>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<128>, gq, dim3(256), 2 * 3 * KT * 128 * 2, stream, a);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<128>, gk, dim3(256), 2 * (4 * QT * 128 * 2 + 2 * QT * 4), stream, a);
+    launch(attn_bwd_dq_kernel<128>, gq, 3 * 3 * KT * 128 * 2, stream, a);
+    launch(attn_bwd_dkv_kernel<128>, gk, 3 * (4 * QT * 128 * 2 + QT * 8), stream, a);
   }
   OTAMD_CHECK_LAUNCH();
   if (qsplit > 1) {
-    int blocks = (int)std::min<long long>((nkv + 255) / 256, 8192);
+    int blocks = (int)std::min<long long>((nkv / 4 + 255) / 256, 8192);
     attn_dkv_cast_kernel<<<blocks, 256, 0, stream>>>(a);
     OTAMD_CHECK_LAUNCH();
   }

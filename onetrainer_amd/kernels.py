@@ -416,8 +416,8 @@ def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None
     a.lddq, a.bsdq = _attn_view(dq, heads)
     a.lddk, a.bsdk = _attn_view(dk, heads)
     a.lddv, a.bsdv = _attn_view(dv, heads)
-    nrow = a.B * a.H * a.Nq
-    nbytes = (nrow + 4) * 4 + 2 * a.B * a.Nk * a.H * a.Dv * 4
+    nbytes = lib().otamd_attn_bwd_ws_bytes(C.byref(a))
+    _req(nbytes > 0, "attention workspace query")
     ws = workspace(nbytes, q.device)
     check(lib().otamd_attn_bwd(C.byref(a), _p(ws), nbytes, stream_handle()), "otamd_attn_bwd")
     return dq, dk, dv
