@@ -70,6 +70,9 @@ int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_byt
 /* plan query: workspace bytes otamd_gemm needs for `splits` (0 = automatic tile + split-K plan) */
 long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out);
 
+/* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves */
+int otamd_gemm_plan_tile(const GemmArgs* in, int splits);
+
 /* replaces: ABI check */
 int otamd_gemm_args_size(void);
 

@@ -350,10 +350,13 @@ static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = fa
   for (int t = 0; t < 4; ++t) {
     if (ft != -3 && t - 1 != ft) continue;
     if (v2_only && t == 0) continue;
-    for (int s = 1; s <= max_splits; s *= 2) {
+    int prev_se = 0;
+    for (int s = 1; s <= max_splits; ++s) {   // every split count (3 and 5 often fill the chip best)
       const long long kps = ((long long)(K + s - 1) / s + 63) / 64 * 64;
       if (s > 1 && kps < 256) break;
       const int se = (int)((K + kps - 1) / kps);
+      if (se == prev_se) continue;
+      prev_se = se;
       const long long tiles = (long long)((M + bm[t] - 1) / bm[t]) * ((N + bn[t] - 1) / bn[t]) * se;
       const long long slots = 256LL * per_cu[t];
       const long long waves = (tiles + slots - 1) / slots;
@@ -377,6 +380,39 @@ OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_
   if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT).splits;
   if (splits_out) *splits_out = s;
   return s > 1 ? (long long)s * in->M * in->N * 4 : 0;
+}
+
+static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_only);
+
+// the tile otamd_gemm would launch for these arguments and splits (0 = automatic): -1 = v1 128x128,
+// 0 = 256x256, 1 = 256x128, 2 = 128x256 (8 waves), 3 = 256x256 (4 waves)
+OTAMD_API int otamd_gemm_plan_tile(const GemmArgs* in, int splits) {
+  if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -9;
+  const bool v2_only = in->bmode == OPM_CONV_WT;
+  GemmPlan plan = plan_gemm(in->M, in->N, in->K, splits > 0 ? splits : 32, v2_only);
+  if (splits > 0) plan = plan_gemm(in->M, in->N, in->K, 1, v2_only), plan.splits = splits;
+  const long long kps = ((long long)(in->K + plan.splits - 1) / plan.splits + BK - 1) / BK * BK;
+  return resolve_tile(*in, (int)((in->K + kps - 1) / kps), plan, v2_only);
+}
+
+// explicit splits: pick the best tile for them; OTAMD_GEMM_TILE overrides; conv-weight B needs v2
+static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_only) {
+  int tile = plan.tile;
+  if (splits > 1 && forced_tile() == -3) {
+    tile = -1;
+    double bt = 1e300;
+    const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, pc[4] = {2, 1, 1, 1};
+    const double rate[4] = {0.55, 1.0, 0.85, 0.85};
+    for (int t = v2_only ? 1 : 0; t < 4; ++t) {
+      const long long tiles = (long long)((a.M + bm[t] - 1) / bm[t]) * ((a.N + bn[t] - 1) / bn[t]) * splits;
+      const double c = (double)((tiles + 256LL * pc[t] - 1) / (256LL * pc[t])) * bm[t] * bn[t] / rate[t] * pc[t];
+      if (c < bt * 0.98) { bt = c; tile = t - 1; }
+    }
+  } else if (forced_tile() != -3) {
+    tile = forced_tile();
+  }
+  if (v2_only && tile < 0) tile = 0;
+  return tile;
 }
 
 OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_bytes, hipStream_t stream) {
@@ -408,21 +444,7 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
   } else {
     a.slab = nullptr;
   }
-  int tile = plan.tile;
-  if (splits > 1 && forced_tile() == -3) {   // explicit splits: pick the best tile for them
-    tile = -1;
-    double bt = 1e300;
-    const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, pc[4] = {2, 1, 1, 1};
-    const double rate[4] = {0.55, 1.0, 0.85, 0.85};
-    for (int t = v2_only ? 1 : 0; t < 4; ++t) {
-      const long long tiles = (long long)((a.M + bm[t] - 1) / bm[t]) * ((a.N + bn[t] - 1) / bn[t]) * splits;
-      const double c = (double)((tiles + 256LL * pc[t] - 1) / (256LL * pc[t])) * bm[t] * bn[t] / rate[t] * pc[t];
-      if (c < bt * 0.98) { bt = c; tile = t - 1; }
-    }
-  } else if (forced_tile() != -3) {
-    tile = forced_tile();
-  }
-  if (v2_only && tile < 0) tile = 0;
+  const int tile = resolve_tile(a, splits, plan, v2_only);
   int rc = OTAMD_EUNSUPPORTED;
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
