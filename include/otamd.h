@@ -45,6 +45,11 @@ typedef struct GemmArgs {
   float* slab;
   int k_per_split;
   ConvGeom ga, gb;
+  /* optional second K segment [K1, K1+K2): A2 K-mode, B2 K-mode (or MN-mode when B is); LoRA up/down fused
+     into the base GEMM (replaces the extra GEMM + add of LoRAModule.forward, modules/module/LoRAModule.py:318-322) */
+  const void* A2; long long lda2;
+  const void* B2; long long ldb2;
+  int K1, K2;
 } GemmArgs;
 
 typedef struct AttnArgs {
@@ -144,6 +149,14 @@ int otamd_conv_weight_transpose(const void* w, void* wt, int Cout, int KK, int C
 
 /* replaces: fp32 reduction result -> bf16/f32 grad (internal) */
 int otamd_cast_f32(const float* x, void* y, long long n, int dst_f32, int accumulate, hipStream_t s);
+
+/* replaces: the per-forward autocast casts of every LoRA down/up weight (LoRAModule.forward under
+   autocast, modules/module/LoRAModule.py:318-322) -- one launch refreshes all bf16 shadows.
+   table: device array of {long long src, dst; int rows, cols, dst_ld; float scale} */
+int otamd_lora_shadow(const float* src, void* dst, const void* table, int n_entries, hipStream_t s);
+
+/* replaces: ABI check */
+int otamd_lora_shadow_entry_size(void);
 
 /* replaces: diffusers get_timestep_embedding (UNet time_proj / add_time_proj) */
 int otamd_timestep_embedding(const float* t, int n, int dim, void* out, long long ldo, hipStream_t s);

@@ -29,7 +29,9 @@ class GemmArgs(C.Structure):
                 ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("alpha", C.c_float),
                 ("bias", C.c_void_p), ("rowvec", C.c_void_p), ("ldv", C.c_longlong), ("rows_per_vec", C.c_int),
                 ("residual", C.c_void_p), ("ldr", C.c_longlong), ("slab", C.c_void_p), ("k_per_split", C.c_int),
-                ("ga", ConvGeom), ("gb", ConvGeom)]
+                ("ga", ConvGeom), ("gb", ConvGeom),
+                ("A2", C.c_void_p), ("lda2", C.c_longlong), ("B2", C.c_void_p), ("ldb2", C.c_longlong),
+                ("K1", C.c_int), ("K2", C.c_int)]
 
 
 class AdamwGroup(C.Structure):
@@ -40,6 +42,11 @@ class AdamwGroup(C.Structure):
 
 class NormChunk(C.Structure):
     _fields_ = [("begin", C.c_longlong), ("end", C.c_longlong), ("tensor", C.c_int), ("pad", C.c_int)]
+
+
+class LoraShadowEntry(C.Structure):
+    _fields_ = [("src", C.c_longlong), ("dst", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
+                ("dst_ld", C.c_int), ("scale", C.c_float)]
 
 
 class AttnArgs(C.Structure):
@@ -89,6 +96,8 @@ SIGNATURES: dict[str, list] = {
     "otamd_colsum_ws_floats": [I, I, I],
     "otamd_conv_weight_transpose": [VP, VP, I, I, I, VP],
     "otamd_cast_f32": [VP, VP, LL, I, I, VP],
+    "otamd_lora_shadow": [VP, VP, VP, I, VP],
+    "otamd_lora_shadow_entry_size": [],
     "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
     "otamd_add": [VP, VP, VP, LL, VP],
     # diffusion.hip
@@ -129,3 +138,4 @@ def check_layouts():
     assert L.otamd_gemm_args_size() == C.sizeof(GemmArgs), (L.otamd_gemm_args_size(), C.sizeof(GemmArgs))
     assert L.otamd_conv_geom_size() == C.sizeof(ConvGeom)
     assert L.otamd_attn_args_size() == C.sizeof(AttnArgs), (L.otamd_attn_args_size(), C.sizeof(AttnArgs))
+    assert L.otamd_lora_shadow_entry_size() == C.sizeof(LoraShadowEntry)

@@ -188,6 +188,20 @@ __global__ void conv_wt_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict_
   }
 }
 
+// LoRA bf16 shadow refresh (one launch per step for every adapter): entry e copies a [rows x cols]
+// fp32 block at src + e.src (contiguous) to bf16 at dst + e.dst with row stride e.dst_ld, times
+// e.scale (alpha / rank for up projections; fused q|k|v ups land on the diagonal of one [3C x 3r]).
+struct LoraShadowEntry { long long src, dst; int rows, cols, dst_ld; float scale; };
+__global__ void __launch_bounds__(256) lora_shadow_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
+                                                          const LoraShadowEntry* __restrict__ tab) {
+  const LoraShadowEntry e = tab[blockIdx.y];
+  const long long n = (long long)e.rows * e.cols;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / e.cols, c = i - r * e.cols;
+    dst[e.dst + r * e.dst_ld + c] = f2bf(src[e.src + i] * e.scale);
+  }
+}
+
 // fp32 -> bf16 / f32 destination, optionally accumulating (grad writes of bias / norm params)
 __global__ void cast_f2b_kernel(const float* __restrict__ x, void* __restrict__ y, long long n, int dst_f32, int acc) {
   GRID_STRIDE(i, n) {
@@ -313,6 +327,14 @@ OTAMD_API int otamd_conv_weight_transpose(const void* w, void* wt, int Cout, int
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
+OTAMD_API int otamd_lora_shadow(const float* src, void* dst, const void* table, int n_entries, hipStream_t s) {
+  if (!src || !dst || !table || n_entries < 0 || n_entries > 65535) return OTAMD_EINVAL;
+  if (n_entries == 0) return OTAMD_OK;
+  lora_shadow_kernel<<<dim3(16, n_entries), 256, 0, s>>>(src, (bf16_t*)dst, (const LoraShadowEntry*)table);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_lora_shadow_entry_size(void) { return (int)sizeof(LoraShadowEntry); }
 OTAMD_API int otamd_cast_f32(const float* x, void* y, long long n, int dst_f32, int accumulate, hipStream_t s) {
   if (!x || !y || n < 0) return OTAMD_EINVAL;
   if (n == 0) return OTAMD_OK;

@@ -29,6 +29,12 @@ struct GemmArgs {
   float* slab;                                                 // split-K partials [splits][M][N]
   int k_per_split;
   ConvGeom ga, gb;
+  // optional second K segment (v2 tiles; LoRA fused into its base GEMM): k in [K1, K1+K2) reads
+  // A2[m][k-K1] (K-mode) and B2 (K-mode [N][K2] when B is K-mode, MN-mode [K2][N] when B is MN-mode).
+  // K == K1 + K2, K1 % 64 == 0.  A2 == nullptr: single segment (K1, K2 ignored).
+  const bf16_t* A2; long long lda2;
+  const bf16_t* B2; long long ldb2;
+  int K1, K2;
 };
 
 

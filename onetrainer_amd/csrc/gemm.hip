@@ -377,7 +377,7 @@ static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = fa
 OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out) {
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -1;
   int s = splits;
-  if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT).splits;
+  if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT || in->A2 != nullptr).splits;
   if (splits_out) *splits_out = s;
   return s > 1 ? (long long)s * in->M * in->N * 4 : 0;
 }
@@ -388,7 +388,7 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
 // 0 = 256x256, 1 = 256x128, 2 = 128x256 (8 waves), 3 = 256x256 (4 waves)
 OTAMD_API int otamd_gemm_plan_tile(const GemmArgs* in, int splits) {
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -9;
-  const bool v2_only = in->bmode == OPM_CONV_WT;
+  const bool v2_only = in->bmode == OPM_CONV_WT || in->A2 != nullptr;
   GemmPlan plan = plan_gemm(in->M, in->N, in->K, splits > 0 ? splits : 32, v2_only);
   if (splits > 0) plan = plan_gemm(in->M, in->N, in->K, 1, v2_only), plan.splits = splits;
   const long long kps = ((long long)(in->K + plan.splits - 1) / plan.splits + BK - 1) / BK * BK;
@@ -419,7 +419,13 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
   if (!in) return OTAMD_EINVAL;
   GemmArgs a = *in;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
-  const bool v2_only = a.bmode == OPM_CONV_WT;
+  const bool v2_only = a.bmode == OPM_CONV_WT || a.A2 != nullptr;
+  if (a.A2) {   // second K segment (LoRA fusion): forms and alignment the v2 kernels support
+    if (!a.B2 || a.K1 <= 0 || a.K2 <= 0 || a.K1 % 64 || a.K != a.K1 + a.K2) return OTAMD_EINVAL;
+    if (!((a.amode == OPM_K || a.amode == OPM_CONV_FWD) && a.bmode == OPM_K) && !(a.amode == OPM_K && a.bmode == OPM_MN))
+      return OTAMD_EUNSUPPORTED;
+    if ((a.lda2 % 8) || (a.ldb2 % 8) || (a.K2 % 8) || !aligned16(a.A2) || !aligned16(a.B2)) return OTAMD_EINVAL;
+  }
   GemmPlan plan = plan_gemm(a.M, a.N, a.K, splits > 0 ? splits : 32, v2_only);
   if (splits > 0) plan = plan_gemm(a.M, a.N, a.K, 1, v2_only), plan.splits = splits;
   splits = plan.splits;
@@ -449,7 +455,7 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
   if (rc != OTAMD_OK) {
-    if (!fn) return rc;
+    if (!fn || a.A2) return rc;   // v1 has no conv-weight B and no second K segment
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid(tiles, 1, splits);
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);

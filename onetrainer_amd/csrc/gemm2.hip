@@ -193,8 +193,9 @@ __device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
 // NW = 8: 2 waves/SIMD (<= 256 VGPRs), wave tiles 128x64 / 64x64.  NW = 4: 1 wave/SIMD (512-entry
 // unified VGPR/AGPR file), 256x256 as 2x2 wave tiles of 128x128 -- a third less LDS read traffic
 // per MFMA (one 16x16x32 fragment read per 4 MFMAs instead of per 2.7).
-template <int AM, int BMODE, int BM, int BN, int NW>
-__global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes) {
+template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2>
+__global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
+                                                                 unsigned a2_bytes, unsigned b2_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int WN = NW == 4 ? 2 : ((BM == 256 && BN == 128) ? 2 : 4);
   constexpr int WM = NW / WN;
@@ -223,6 +224,27 @@ __global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, u
   Stage<BMODE, BN, NW> sb;
   sa.prepare(args.ga, args.lda, m0, args.M, wave, lane);
   sb.prepare(args.gb, args.ldb, n0, args.N, wave, lane);
+  // second K segment: A2 always K-mode; B2 in the LDS image mode of B
+  constexpr int B2M = BKm ? OPM_K : OPM_MN;
+  Stage<OPM_K, SEG2 ? BM : 64 * NW / 8, NW> sa2;
+  Stage<B2M, SEG2 ? BN : 64 * NW / 8, NW> sb2;
+  __amdgpu_buffer_rsrc_t ra2 = ra, rb2 = rb;
+  if constexpr (SEG2) {
+    ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)args.A2, (short)0, (int)a2_bytes, 0x00020000);
+    rb2 = __builtin_amdgcn_make_buffer_rsrc((void*)args.B2, (short)0, (int)b2_bytes, 0x00020000);
+    sa2.prepare(args.ga, args.lda2, m0, args.M, wave, lane);
+    sb2.prepare(args.gb, args.ldb2, n0, args.N, wave, lane);
+  }
+  // K tile at k0 (never straddles K1: K1 % 64 == 0) into the stage at img
+  auto issue_tile = [&](char* img, int k0) {
+    if (!SEG2 || k0 < args.K1) {
+      sa.issue(ra, img, args.ga, args.lda, k0, SEG2 ? args.K1 : kend, wave);
+      sb.issue(rb, img + ABYTES, args.gb, args.ldb, k0, SEG2 ? args.K1 : kend, wave);
+    } else {
+      sa2.issue(ra2, img, args.ga, args.lda2, k0 - args.K1, args.K2, wave);
+      sb2.issue(rb2, img + ABYTES, args.gb, args.ldb2, k0 - args.K1, args.K2, wave);
+    }
+  };
 
   const int wm = wave / WN, wn = wave % WN;
   float4v acc[MI][NJ];
@@ -263,11 +285,9 @@ __global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, u
   //   phase B: MFMA(h1 of tile k) || ds_read(h0 of tile k+1)
   bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
   if (nk > 0) {
-    sa.issue(ra, smem, args.ga, args.lda, kbeg, kend, wave);
-    sb.issue(rb, smem + ABYTES, args.gb, args.ldb, kbeg, kend, wave);
+    issue_tile(smem, kbeg);
     if (nk > 1) {
-      sa.issue(ra, smem + STAGE, args.ga, args.lda, kbeg + 64, kend, wave);
-      sb.issue(rb, smem + STAGE + ABYTES, args.gb, args.ldb, kbeg + 64, kend, wave);
+      issue_tile(smem + STAGE, kbeg + 64);
       wait_vmcnt<LOADS>();
     } else {
       wait_vmcnt<0>();
@@ -289,11 +309,7 @@ __global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, u
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wait_vmcnt<0>();       // tile k+1 (the only DMA in flight) has landed
     BARRIER();
-    if (kt + 2 < nk) {
-      char* nb = smem + (kt & 1) * STAGE;
-      sa.issue(ra, nb, args.ga, args.lda, kbeg + (kt + 2) * 64, kend, wave);
-      sb.issue(rb, nb + ABYTES, args.gb, args.ldb, kbeg + (kt + 2) * 64, kend, wave);
-    }
+    if (kt + 2 < nk) issue_tile(smem + (kt & 1) * STAGE, kbeg + (kt + 2) * 64);
     // phase B
     __builtin_amdgcn_sched_barrier(0);
     {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
@@ -350,11 +366,17 @@ __global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, u
   }
 }
 
-typedef void (*gemm2_fn)(GemmArgs, unsigned, unsigned);
+typedef void (*gemm2_fn)(GemmArgs, unsigned, unsigned, unsigned, unsigned);
 
 template <int BM, int BN, int NW>
-static gemm2_fn pick2(int am, int bm) {
-#define CASE2(a, b) if (am == a && bm == b) return gemm2_kernel<a, b, BM, BN, NW>;
+static gemm2_fn pick2(int am, int bm, bool seg2) {
+  if (seg2) {   // LoRA-fused forms: linear fwd, conv fwd, linear dgrad
+    if (am == OPM_K && bm == OPM_K) return gemm2_kernel<OPM_K, OPM_K, BM, BN, NW, true>;
+    if (am == OPM_CONV_FWD && bm == OPM_K) return gemm2_kernel<OPM_CONV_FWD, OPM_K, BM, BN, NW, true>;
+    if (am == OPM_K && bm == OPM_MN) return gemm2_kernel<OPM_K, OPM_MN, BM, BN, NW, true>;
+    return nullptr;
+  }
+#define CASE2(a, b) if (am == a && bm == b) return gemm2_kernel<a, b, BM, BN, NW, false>;
   CASE2(OPM_K, OPM_K)
   CASE2(OPM_K, OPM_MN)
   CASE2(OPM_MN, OPM_MN)
@@ -383,17 +405,26 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   if (ab <= 0 || bb <= 0 || ab >= 0x7fff0000LL || bb >= 0x7fff0000LL) return OTAMD_EUNSUPPORTED;
   gemm2_fn fn = nullptr;
   int BMv = 256, BNv = 256, NWv = 8;
-  if (tile == 0) fn = pick2<256, 256, 8>(a.amode, a.bmode);
-  else if (tile == 1) { fn = pick2<256, 128, 8>(a.amode, a.bmode); BNv = 128; }
-  else if (tile == 2) { fn = pick2<128, 256, 8>(a.amode, a.bmode); BMv = 128; }
-  else { fn = pick2<256, 256, 4>(a.amode, a.bmode); NWv = 4; }
+  const bool seg2 = a.A2 != nullptr;
+  unsigned a2b = 0, b2b = 0;
+  if (seg2) {
+    const long long x = ((long long)(a.M - 1) * a.lda2 + a.K2) * 2;
+    const long long y = a.bmode == OPM_K ? ((long long)(a.N - 1) * a.ldb2 + a.K2) * 2 : ((long long)(a.K2 - 1) * a.ldb2 + a.N) * 2;
+    if (x <= 0 || y <= 0 || x >= 0x7fff0000LL || y >= 0x7fff0000LL) return OTAMD_EUNSUPPORTED;
+    a2b = (unsigned)x;
+    b2b = (unsigned)y;
+  }
+  if (tile == 0) fn = pick2<256, 256, 8>(a.amode, a.bmode, seg2);
+  else if (tile == 1) { fn = pick2<256, 128, 8>(a.amode, a.bmode, seg2); BNv = 128; }
+  else if (tile == 2) { fn = pick2<128, 256, 8>(a.amode, a.bmode, seg2); BMv = 128; }
+  else if (!seg2) { fn = pick2<256, 256, 4>(a.amode, a.bmode, false); NWv = 4; }
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
   const int lds = 2 * (BMv + BNv) * 128;
   static bool attr_set[3] = {false, false, false};
   (void)attr_set;
   hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(fn, dim3(tiles, 1, splits), dim3(NWv * 64), lds, stream, a, (unsigned)ab, (unsigned)bb);
+  hipLaunchKernelGGL(fn, dim3(tiles, 1, splits), dim3(NWv * 64), lds, stream, a, (unsigned)ab, (unsigned)bb, a2b, b2b);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

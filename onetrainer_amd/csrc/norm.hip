@@ -480,7 +480,8 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
                                   long long lddx, int rows, int C, const void* gamma, const float* mean,
                                   const float* rstd, void* dgamma, void* dbeta, int param_f32, int param_acc,
                                   float* part, int accumulate, hipStream_t stream) {
-  if (!x || !dy || !dx || !gamma || !mean || !rstd || !dgamma || !dbeta || !part) return OTAMD_EINVAL;
+  // dgamma == dbeta == nullptr: frozen affine (LoRA training), no parameter-gradient reduce
+  if (!x || !dy || !dx || !gamma || !mean || !rstd || (!dgamma != !dbeta) || !part) return OTAMD_EINVAL;
   if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8 || lddx % 8) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)gamma) & 15) return OTAMD_EINVAL;
   int nb = (rows + 3) / 4;
@@ -489,6 +490,7 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
                                                             (bf16_t*)dx, lddx, rows, C, (const bf16_t*)gamma, mean,
                                                             rstd, part, accumulate);
   OTAMD_CHECK_LAUNCH();
+  if (!dgamma) return OTAMD_OK;
   ln_param_reduce_kernel<<<(2 * C + 31) / 32, 256, 0, stream>>>(part, nb, C, dgamma, dbeta, param_f32, param_acc);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;

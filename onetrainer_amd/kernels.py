@@ -105,9 +105,26 @@ def _out(out, M, N, dtype, device):
     return out
 
 
+def _seg2(a, t: torch.Tensor, b2: torch.Tensor, k1: int, b2_mn: bool) -> bool:
+    """attach the second K segment (LoRA fused into its base GEMM): A2 = t [M, r] (K-mode),
+    B2 = b2 ([N, r] K-mode, or [r, N] MN-mode when b2_mn).  False if the split point is not
+    64-aligned (caller then issues the LoRA product as a separate accumulate GEMM)."""
+    r = t.shape[1]
+    if k1 % 64 or r % 8:
+        return False
+    _req(t.dtype == BF16 and b2.dtype == BF16 and _aligned(t) and _aligned(b2), "LoRA operands bf16, aligned")
+    _req((b2.shape[0] == r) if b2_mn else (b2.shape[1] == r), "LoRA operand shapes")
+    a.A2, a.lda2 = _p(t), _ld_rows(t)
+    a.B2, a.ldb2 = _p(b2), _ld_rows(b2)
+    a.K1, a.K2 = k1, r
+    a.K = k1 + r
+    return True
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, rowvec=None, rows_per_vec=0,
-           out=None, out_dtype=BF16, alpha=1.0, accumulate=False) -> torch.Tensor:
-    """y[M,N] = alpha * x[M,K] @ w[N,K]^T (+bias[N]) (+rowvec[m//rows_per_vec]) (+residual)."""
+           out=None, out_dtype=BF16, alpha=1.0, accumulate=False, lora=None) -> torch.Tensor:
+    """y[M,N] = alpha * x[M,K] @ w[N,K]^T (+bias[N]) (+rowvec[m//rows_per_vec]) (+residual).
+    lora = (t [M,r], b2 [N,r]): y += t @ b2^T, fused into the same GEMM as a second K segment."""
     _req(x.dtype == BF16 and w.dtype == BF16 and x.is_cuda, "linear: bf16 cuda tensors")
     M, K = x.shape
     N, K2 = w.shape
@@ -120,12 +137,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, rowvec=No
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), out.stride(0) if M > 1 else N, int(out.dtype == F32), int(accumulate)
     a.M, a.N, a.K, a.alpha = M, N, K, alpha
     _epilogue(a, bias, rowvec, rows_per_vec, residual, M, N)
+    fused = lora is not None and _seg2(a, lora[0], lora[1], K, False)
     _gemm(a, 0, x.device)
+    if lora is not None and not fused:
+        linear(lora[0], lora[1], out=out, accumulate=True)
     return out
 
 
-def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, accumulate=False) -> torch.Tensor:
-    """dx[M,K] = dy[M,N] @ w[N,K]."""
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, accumulate=False,
+                 lora=None) -> torch.Tensor:
+    """dx[M,K] = dy[M,N] @ w[N,K].  lora = (u [M,r], a2 [r,K]): dx += u @ a2 (second K segment)."""
     _req(dy.dtype == BF16 and w.dtype == BF16, "linear_dgrad: bf16")
     M, N = dy.shape
     N2, K = w.shape
@@ -137,12 +158,16 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, acc
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), out.stride(0) if M > 1 else K, int(out.dtype == F32), int(accumulate)
     a.M, a.N, a.K = M, K, N
     _epilogue(a, None, None, 0, residual, M, K)
+    fused = lora is not None and _seg2(a, lora[0], lora[1], N, True)
     _gemm(a, 0, dy.device)
+    if lora is not None and not fused:
+        linear_dgrad(lora[0], lora[1], out=out, accumulate=True)
     return out
 
 
-def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out=None, accumulate=False, splits=None) -> torch.Tensor:
-    """dw[N,K] = dy[T,N]^T @ x[T,K]  (split-K over tokens T, deterministic slab reduce)."""
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out=None, accumulate=False, splits=None,
+                 alpha=1.0) -> torch.Tensor:
+    """dw[N,K] = alpha * dy[T,N]^T @ x[T,K]  (split-K over tokens T, deterministic slab reduce)."""
     _req(dy.dtype == BF16 and x.dtype == BF16, "linear_wgrad: bf16")
     T, N = dy.shape
     T2, K = x.shape
@@ -152,7 +177,7 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out=None, accumulate=False, 
     a.A, a.lda, a.amode = _p(dy), _ld_rows(dy), OPM_MN
     a.B, a.ldb, a.bmode = _p(x), _ld_rows(x), OPM_MN
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), out.stride(0), int(out.dtype == F32), int(accumulate)
-    a.M, a.N, a.K = N, K, T
+    a.M, a.N, a.K, a.alpha = N, K, T, alpha
     _gemm(a, splits or 0, dy.device)
     return out
 
@@ -182,7 +207,7 @@ def _nhwc(x: torch.Tensor):
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, pad=1, upsample=False, residual=None,
-           rowvec=None, out=None) -> torch.Tensor:
+           rowvec=None, out=None, lora=None) -> torch.Tensor:
     """NHWC conv: y[n,p,q,co] = sum w[co,r,s,ci] * x[n, p*st+r-pad, q*st+s-pad, ci] (+bias, +rowvec[n], +residual).
     upsample=True reads x through a nearest-2x upsample (diffusers Upsample2D)."""
     N, H, W, Cin, ldx = _nhwc(x)
@@ -202,11 +227,16 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, pad=1, upsampl
     a.M, a.N, a.K = M, Cout, KH * KW * Cin
     res2 = residual.reshape(M, Cout) if residual is not None else None
     _epilogue(a, bias, rowvec, P * Q if rowvec is not None else 0, res2, M, Cout)
+    t2 = lora[0].reshape(M, lora[0].shape[-1]) if lora is not None else None
+    fused = lora is not None and _seg2(a, t2, lora[1], KH * KW * Cin, False)
     _gemm(a, 0, x.device)
+    if lora is not None and not fused:
+        linear(t2, lora[1], out=out.view(M, Cout), accumulate=True)
     return out
 
 
-def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw, stride=1, pad=1, out=None) -> torch.Tensor:
+def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw, stride=1, pad=1, out=None,
+                 accumulate=False) -> torch.Tensor:
     """dx of conv2d (no upsample): dx[n,h,w,ci] = sum_{r,s,co} dy[n,(h+pad-r)/st,(w+pad-s)/st,co] * w[co,r,s,ci].
     w is the stored weight [Cout][KH][KW][Cin], read in place (OPM_CONV_WT: no transpose pass)."""
     N, P, Q, Cout, ldy = _nhwc(dy)
@@ -222,7 +252,7 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw, stride=1, pad=1, out=
     a.ga = _geom(N, P, Q, Cout, H, W, KH, KW, stride, pad, False, ldy)
     a.B, a.ldb, a.bmode = _p(w), Cin, OPM_CONV_WT
     a.gb = _geom(N, P, Q, Cout, H, W, KH, KW, stride, pad, False, Cin)
-    a.C, a.ldc = _p(out), Cin
+    a.C, a.ldc, a.accumulate = _p(out), Cin, int(accumulate)
     a.M, a.N, a.K = N * H * W, Cin, KH * KW * Cout
     _gemm(a, 0, dy.device)
     return out
@@ -351,19 +381,21 @@ def layernorm_fwd(x, gamma, beta, eps, out=None):
     return out, (mean, rstd)
 
 
-def layernorm_bwd(x, dy, gamma, stats, dx=None, accumulate=False, dgamma=None, dbeta=None, param_acc=False):
+def layernorm_bwd(x, dy, gamma, stats, dx=None, accumulate=False, dgamma=None, dbeta=None, param_acc=False,
+                  need_param_grads=True):
     rows, C_, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
     if dx is None:
         dx = torch.empty(x.shape, dtype=BF16, device=x.device)
     _, _, lddx = _rows2d(dx)
-    if dgamma is None:
+    if dgamma is None and need_param_grads:
         dgamma = torch.empty(C_, dtype=F32, device=x.device)
         dbeta = torch.empty(C_, dtype=F32, device=x.device)
     part = workspace(1024 * 2 * C_ * 4, x.device)
     mean, rstd = stats
     check(lib().otamd_layernorm_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, rows, C_, _p(gamma), _p(mean), _p(rstd),
-                                    _p(dgamma), _p(dbeta), int(dgamma.dtype == F32), int(param_acc), _p(part),
+                                    _p(dgamma), _p(dbeta), int(dgamma is not None and dgamma.dtype == F32),
+                                    int(param_acc), _p(part),
                                     int(accumulate), stream_handle()), "otamd_layernorm_bwd")
     return dx, dgamma, dbeta
 
@@ -508,6 +540,14 @@ def conv_weight_transpose(w):
     check(lib().otamd_conv_weight_transpose(_p(w), _p(wt), Cout, KH * KW, Cin, stream_handle()),
           "otamd_conv_weight_transpose")
     return wt
+
+
+def lora_shadow(src_f32: torch.Tensor, dst_bf16: torch.Tensor, table: torch.Tensor, n_entries: int):
+    """refresh every LoRA bf16 shadow from the fp32 store in one launch (table: device bytes of
+    _lib.LoraShadowEntry[n_entries])."""
+    _req(src_f32.dtype == F32 and dst_bf16.dtype == BF16 and table.dtype == torch.uint8, "lora shadow dtypes")
+    check(lib().otamd_lora_shadow(_p(src_f32), _p(dst_bf16), _p(table), n_entries, stream_handle()),
+          "otamd_lora_shadow")
 
 
 def cast_f32_bf16(x, out=None, accumulate=False):

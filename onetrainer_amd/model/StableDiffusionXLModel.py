@@ -40,6 +40,12 @@ class StableDiffusionXLModel:
         self.param_group_mapping = None
         self.ema = None
         self.train_progress = TrainProgress()
+        self.unet_lora = None     # LoRAUNetWrapper (StableDiffusionXLLoRASetup.setup_model)
+
+    @property
+    def train_store(self):
+        """the FlatParamStore the optimizer / grad norm / DP reducer run over."""
+        return self.unet_lora.store if self.unet_lora is not None else self.unet.store
 
     def combine_text_encoder_output(self, te1, te2, pooled):
         """concat on the last dim (StableDiffusionXLModel.py:288-295) -> [B, 77, 768+1280]."""

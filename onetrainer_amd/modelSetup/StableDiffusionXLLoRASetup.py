@@ -1,0 +1,68 @@
+"""LoRA plugin (mirrors modules/modelSetup/StableDiffusionXLLoRASetup.py:19-220): frozen bf16 UNet,
+fp32 adapters on every Linear/Conv2d matching `lora_layers` (module/lora.py), parameter group
+"unet_lora" (:66-72), fused fp32 AdamW over the adapter store (create.py:509-534 with
+lora_weight_dtype FLOAT_32), shadow refresh after each update (the reference re-casts under
+autocast on every forward)."""
+from __future__ import annotations
+
+import torch
+
+from ..module.lora import PRESETS, LoRAUNetWrapper
+from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
+from ..util.optimizer.adamw_fused import FusedAdamW
+from .BaseStableDiffusionXLSetup import BaseStableDiffusionXLSetup
+
+
+class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
+    def create_parameters(self, model, config) -> NamedParameterGroupCollection:
+        pgc = NamedParameterGroupCollection()
+        if config.text_encoder.train or config.text_encoder_2.train:
+            raise NotImplementedError("text-encoder LoRA is outside this build's hot path (text is cached)")
+        if config.unet.train:
+            pgc.add_group(NamedParameterGroup("unet_lora", model.unet_lora.parameters(),
+                                              config.unet.learning_rate))
+        return pgc
+
+    def setup_optimizations(self, model, config):
+        model.train_dtype = torch.bfloat16
+
+    @staticmethod
+    def layer_filter(config):
+        if config.lora_layers:
+            return config.lora_layers.split(",")
+        return PRESETS.get(config.lora_layer_preset or "full", [])
+
+    def setup_model(self, model, config):
+        if getattr(config, "lora_decompose", False) or config.peft_type != "LORA":
+            raise NotImplementedError("DoRA / LoHa are not on this build's hot path")
+        if config.dropout_probability and config.dropout_probability > 0:
+            raise NotImplementedError("LoRA dropout > 0 is not on this build's hot path")
+        if model.unet.store.trainable:
+            raise ValueError("LoRA training needs a frozen base UNet (create_model(..., training_method='LORA'))")
+        self.setup_optimizations(model, config)
+        if model.unet_lora is None:
+            model.unet_lora = LoRAUNetWrapper(model.unet, rank=config.lora_rank, alpha=config.lora_alpha,
+                                              module_filter=self.layer_filter(config), seed=0)
+        model.unet.lora = model.unet_lora
+        params = self.create_parameters(model, config)
+        model.parameters = params
+        oc = config.optimizer
+        if oc.optimizer != "ADAMW":
+            raise NotImplementedError(f"optimizer {oc.optimizer}: only ADAMW is on the hot path")
+        model.optimizer = FusedAdamW(model.unet_lora.store, params.parameters_for_optimizer(config),
+                                     lr=config.learning_rate,
+                                     betas=(oc.beta1 if oc.beta1 is not None else 0.9,
+                                            oc.beta2 if oc.beta2 is not None else 0.999),
+                                     eps=oc.eps if oc.eps is not None else 1e-8,
+                                     weight_decay=oc.weight_decay if oc.weight_decay is not None else 1e-2,
+                                     stochastic_rounding=oc.stochastic_rounding)
+        model.param_group_mapping = params.unique_name_mapping()
+
+    def setup_train_device(self, model, config):
+        pass
+
+    def after_optimizer_step(self, model, config, train_progress):
+        model.unet_lora.refresh()
+
+    def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
+        pass

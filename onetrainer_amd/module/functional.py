@@ -28,6 +28,10 @@ class PRef:
         self.g = store.view(self.names, shape, grad=True)
         self.params = tuple(store.params[n] for n in self.names)
 
+    @property
+    def trainable(self) -> bool:
+        return self.store.trainable
+
     def acc(self) -> bool:
         return self.store.accumulate_into(self.names)
 
@@ -79,17 +83,70 @@ class LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.linear_dgrad(dy2, wref.w).view(ctx.xshape)
-        K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
-        wref.done()
-        if bref is not None:
+        if wref.trainable:
+            K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
+            wref.done()
+        if bref is not None and bref.trainable:
             K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
             bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, dres) + (None,) * (len(ctx.needs_input_grad) - 4)
 
 
-def linear(x, wref, bref=None, residual=None):
+def linear(x, wref, bref=None, residual=None, lora=None):
+    if lora is not None:
+        return LoraLinearFn.apply(x, wref, bref, residual, lora, *lora.params, *_trainable_params(wref, bref))
     return LinearFn.apply(x, wref, bref, residual, *_params(wref, bref))
+
+
+def _trainable_params(*refs):
+    return [p for r in refs if r is not None and r.trainable for p in r.params]
+
+
+class LoraLinearFn(torch.autograd.Function):
+    """y = x W^T (+b) (+residual) + s * (x A^T) B^T with a frozen base (LoRAModule.forward,
+    modules/module/LoRAModule.py:318-322).  Forward: t = x A^T (skinny GEMM), then the base GEMM
+    with [t | s B] as its second K segment.  Backward: u = dy (sB); dx = [dy | u] [W ; A] (one
+    GEMM); dA = u^T x; dB_p = s dy_p^T t_p per fused part; all adapter grads fp32."""
+
+    @staticmethod
+    def forward(ctx, x, wref, bref, residual, site, *params):
+        shp = x.shape
+        x2 = _rows(x)
+        r2 = _rows(residual) if residual is not None else None
+        t = K.linear(x2, site.down)
+        y = K.linear(x2, wref.w, bias=bref.w if bref is not None else None, residual=r2, lora=(t, site.up2))
+        ctx.save_for_backward(x2, t)
+        ctx.wref, ctx.bref, ctx.site, ctx.has_res, ctx.xshape = wref, bref, site, residual is not None, shp
+        return y.view(*shp[:-1], wref.w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, t = ctx.saved_tensors
+        wref, bref, site = ctx.wref, ctx.bref, ctx.site
+        dy2 = _rows(dy)
+        if dy2.stride(1) != 1 or dy2.stride(0) % 8:
+            dy2 = dy2.contiguous()
+        u = K.linear_dgrad(dy2, site.up2)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.linear_dgrad(dy2, wref.w, lora=(u, site.down)).view(ctx.xshape)
+        acc = site.acc()
+        K.linear_wgrad(u, x2, out=site.g_down, accumulate=acc)
+        r, n0 = site.rank, 0
+        for p, g in enumerate(site.g_up):
+            n1 = n0 + g.shape[0]
+            K.linear_wgrad(dy2[:, n0:n1], t[:, p * r:(p + 1) * r], out=g, accumulate=acc, alpha=site.scale)
+            n0 = n1
+        site.done()
+        if wref.trainable:
+            K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
+            wref.done()
+        if bref is not None and bref.trainable:
+            K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
+            bref.done()
+        dres = dy if ctx.has_res else None
+        return (dx, None, None, dres, None) + (None,) * (len(ctx.needs_input_grad) - 5)
 
 
 class ConvFn(torch.autograd.Function):
@@ -120,21 +177,78 @@ class ConvFn(torch.autograd.Function):
                 dx = K.upsample2x_bwd(dup)
             else:
                 dx = K.conv2d_dgrad(dy, wref.w, (H, W), ctx.stride, 1)
-        K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
-        wref.done()
+        if wref.trainable:
+            K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
+            wref.done()
         drow = None
         P, Q = dy.shape[1], dy.shape[2]
         if ctx.has_rowvec:
             drow = K.colsum(dy, rows_per_group=P * Q, out=torch.empty((dy.shape[0], dy.shape[3]), dtype=torch.bfloat16,
                                                                        device=dy.device))
-        if bref is not None:
+        if bref is not None and bref.trainable:
             K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
             bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, drow, dres, None, None) + (None,) * (len(ctx.needs_input_grad) - 7)
 
 
-def conv(x, wref, bref=None, rowvec=None, residual=None, stride=1, upsample=False):
+class LoraConvFn(torch.autograd.Function):
+    """ConvFn + LoRA (LoRAModule.py:142-155 conv branch): down = the base 3x3 geometry in->r,
+    up = 1x1 r->out fused into the base conv GEMM as its second K segment; frozen base."""
+
+    @staticmethod
+    def forward(ctx, x, wref, bref, rowvec, residual, stride, upsample, site, *params):
+        t = K.conv2d(x, site.down, stride=stride, pad=1, upsample=upsample)
+        y = K.conv2d(x, wref.w, bias=bref.w if bref is not None else None, stride=stride, pad=1, upsample=upsample,
+                     residual=residual, rowvec=rowvec, lora=(t, site.up2))
+        ctx.save_for_backward(x, t)
+        ctx.wref, ctx.bref, ctx.stride, ctx.upsample, ctx.site = wref, bref, stride, upsample, site
+        ctx.has_rowvec, ctx.has_res = rowvec is not None, residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, t = ctx.saved_tensors
+        wref, bref, site = ctx.wref, ctx.bref, ctx.site
+        if dy.stride(3) != 1 or dy.stride(2) % 8 or dy.stride(1) != dy.stride(2) * dy.shape[2] \
+                or dy.stride(0) != dy.stride(1) * dy.shape[1]:
+            dy = dy.contiguous()
+        N, H, W, _ = x.shape
+        _, P, Q, Cout = dy.shape
+        M = N * P * Q
+        dy2 = dy.reshape(M, Cout)
+        r = site.rank
+        u = K.linear_dgrad(dy2, site.up2).view(N, P, Q, r)          # dy (s B)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.upsample:
+                dup = K.conv2d_dgrad(dy, wref.w, (2 * H, 2 * W), 1, 1)
+                K.conv2d_dgrad(u, site.down, (2 * H, 2 * W), 1, 1, out=dup, accumulate=True)
+                dx = K.upsample2x_bwd(dup)
+            else:
+                dx = K.conv2d_dgrad(dy, wref.w, (H, W), ctx.stride, 1)
+                K.conv2d_dgrad(u, site.down, (H, W), ctx.stride, 1, out=dx, accumulate=True)
+        acc = site.acc()
+        K.conv2d_wgrad(u, x, site.k, ctx.stride, 1, upsample=ctx.upsample, out=site.g_down, accumulate=acc)
+        K.linear_wgrad(dy2, t.reshape(M, r), out=site.g_up[0], accumulate=acc, alpha=site.scale)
+        site.done()
+        if wref.trainable:
+            K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
+            wref.done()
+        drow = None
+        if ctx.has_rowvec:
+            drow = K.colsum(dy, rows_per_group=P * Q, out=torch.empty((N, Cout), dtype=torch.bfloat16, device=dy.device))
+        if bref is not None and bref.trainable:
+            K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
+            bref.done()
+        dres = dy if ctx.has_res else None
+        return (dx, None, None, drow, dres, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 8)
+
+
+def conv(x, wref, bref=None, rowvec=None, residual=None, stride=1, upsample=False, lora=None):
+    if lora is not None:
+        return LoraConvFn.apply(x, wref, bref, rowvec, residual, stride, upsample, lora, *lora.params,
+                                *_trainable_params(wref, bref))
     return ConvFn.apply(x, wref, bref, rowvec, residual, stride, upsample, *_params(wref, bref))
 
 
@@ -149,10 +263,13 @@ class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, *stats = ctx.saved_tensors
-        dx, _, _ = K.groupnorm_bwd(x, dy, ctx.gref.w, ctx.groups, ctx.silu, stats, dgamma=ctx.gref.g,
-                                   dbeta=ctx.bref.g, param_acc=ctx.gref.acc())
-        ctx.gref.done()
-        ctx.bref.done()
+        tr = ctx.gref.trainable
+        dx, _, _ = K.groupnorm_bwd(x, dy, ctx.gref.w, ctx.groups, ctx.silu, stats, dgamma=ctx.gref.g if tr else None,
+                                   dbeta=ctx.bref.g if tr else None, param_acc=tr and ctx.gref.acc(),
+                                   need_param_grads=tr)
+        if tr:
+            ctx.gref.done()
+            ctx.bref.done()
         return (dx if ctx.needs_input_grad[0] else None,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
 
@@ -173,10 +290,13 @@ class LayerNormFn(torch.autograd.Function):
         x, *stats = ctx.saved_tensors
         if dy.stride(-1) != 1:
             dy = dy.contiguous()
-        dx, _, _ = K.layernorm_bwd(x, dy, ctx.gref.w, stats, dgamma=ctx.gref.g, dbeta=ctx.bref.g,
-                                   param_acc=ctx.gref.acc())
-        ctx.gref.done()
-        ctx.bref.done()
+        tr = ctx.gref.trainable
+        dx, _, _ = K.layernorm_bwd(x, dy, ctx.gref.w, stats, dgamma=ctx.gref.g if tr else None,
+                                   dbeta=ctx.bref.g if tr else None, param_acc=tr and ctx.gref.acc(),
+                                   need_param_grads=tr)
+        if tr:
+            ctx.gref.done()
+            ctx.bref.done()
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
 

@@ -27,8 +27,10 @@ class Slot:
 
 
 class FlatParamStore:
-    def __init__(self, specs, dtype, device, align_bytes=16):
-        """specs: iterable of (name, shape, group) in layout order."""
+    def __init__(self, specs, dtype, device, align_bytes=16, trainable=True):
+        """specs: iterable of (name, shape, group) in layout order.  trainable=False: a frozen base
+        (LoRA training, unet.requires_grad_(False) in StableDiffusionXLLoRASetup.py:78-86): no grad
+        buffer, parameters do not require grad, backward kernels skip its weight gradients."""
         esz = torch.tensor([], dtype=dtype).element_size()
         al = max(8, align_bytes // esz)   # >= 8 elements: the grad-norm kernel reads 8-wide chunks
         self.dtype, self.device = dtype, device
@@ -44,13 +46,15 @@ class FlatParamStore:
             self.order.append(name)
             off += n
         self.numel = (off + al - 1) // al * al
+        self.trainable = trainable
         self.data = torch.zeros(self.numel, dtype=dtype, device=device)
-        self.grad = torch.zeros(self.numel, dtype=dtype, device=device)
+        self.grad = torch.zeros(self.numel, dtype=dtype, device=device) if trainable else None
         self.params: dict[str, torch.nn.Parameter] = {}
         for name in self.order:
             s = self.slots[name]
-            p = torch.nn.Parameter(self.data[s.offset:s.offset + s.numel].view(s.shape))
-            p.grad = self.grad[s.offset:s.offset + s.numel].view(s.shape)
+            p = torch.nn.Parameter(self.data[s.offset:s.offset + s.numel].view(s.shape), requires_grad=trainable)
+            if trainable:
+                p.grad = self.grad[s.offset:s.offset + s.numel].view(s.shape)
             self.params[name] = p
         self._written: set[str] = set()
         self.accumulating = False          # True on micro-steps after the first of a GA window
@@ -69,6 +73,8 @@ class FlatParamStore:
                 raise ValueError(f"parameters {names} are not adjacent in the flat store")
             end += s.numel
         buf = self.grad if grad else self.data
+        if buf is None:
+            return None
         v = buf[first.offset:end]
         if shape is not None:
             v = v.view(shape)
@@ -96,7 +102,7 @@ class FlatParamStore:
 
     def finish_backward(self):
         """zero the grads of parameters that received none this micro-step (overwrite semantics)."""
-        if not self.accumulating:
+        if self.trainable and not self.accumulating:
             for n in self.order:
                 if n not in self._written:
                     s = self.slots[n]

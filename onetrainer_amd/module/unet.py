@@ -186,14 +186,16 @@ def _store_shape(name, shape, kind, cfg):
 class UNet2DConditionModel:
     """HIP UNet; parameters live in `self.store` (FlatParamStore)."""
 
-    def __init__(self, cfg: UNetConfig, device, dtype=BF16, seed: int | None = 0, group: str = "unet"):
+    def __init__(self, cfg: UNetConfig, device, dtype=BF16, seed: int | None = 0, group: str = "unet",
+                 trainable: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
         self.specs = unet_specs(cfg)
         self.store = FlatParamStore([(n, _store_shape(n, sh, k, cfg), group) for n, sh, k, _ in self.specs],
-                                    dtype, self.device)
+                                    dtype, self.device, trainable=trainable)
         self._refs: dict = {}
+        self.lora = None      # module/lora.py LoRAUNetWrapper when training adapters on a frozen base
         if seed is not None:
             self.init_weights(seed)
 
@@ -268,8 +270,25 @@ class UNet2DConditionModel:
         return r
 
     # ----- blocks -------------------------------------------------------------------------------
+    def _lo(self, module: str):
+        """the LoRA site of a base module (None without adapters or when the filter excludes it)."""
+        return self.lora.site_of.get(module) if self.lora is not None else None
+
+    def _lo_fused(self, modules):
+        """site of a fused base GEMM (to_q|to_k|to_v, to_k|to_v): all parts adapted or none."""
+        sites = [self._lo(m) for m in modules]
+        if all(s is None for s in sites):
+            return None
+        if any(s is None or s.modules != list(modules) for s in sites):
+            raise NotImplementedError(f"LoRA layer filter adapts only part of the fused projection {modules}")
+        return sites[0]
+
     def _linear(self, x, p, bias=True, residual=None):
-        return Fn.linear(x, self.R(p + ".weight"), self.R(p + ".bias") if bias else None, residual)
+        return Fn.linear(x, self.R(p + ".weight"), self.R(p + ".bias") if bias else None, residual, lora=self._lo(p))
+
+    def _conv(self, x, p, rowvec=None, residual=None, stride=1, upsample=False):
+        return Fn.conv(x, self.R(p + ".weight"), self.R(p + ".bias"), rowvec=rowvec, residual=residual, stride=stride,
+                       upsample=upsample, lora=self._lo(p))
 
     def _gn(self, x, p, silu, eps=None):
         cfg = self.cfg
@@ -280,25 +299,25 @@ class UNet2DConditionModel:
         cin = x.shape[-1]
         h = self._gn(x, p + ".norm1", True)
         tp = self._linear(semb, p + ".time_emb_proj")
-        h = Fn.conv(h, self.R(p + ".conv1.weight"), self.R(p + ".conv1.bias"), rowvec=tp)
+        h = self._conv(h, p + ".conv1", rowvec=tp)
         h = self._gn(h, p + ".norm2", True)
         sc = x
         if (p + ".conv_shortcut.weight") in self.store.slots:
             sc = self._linear(x, p + ".conv_shortcut")
-        return Fn.conv(h, self.R(p + ".conv2.weight"), self.R(p + ".conv2.bias"), residual=sc)
+        return self._conv(h, p + ".conv2", residual=sc)
 
     def _block(self, h, p, C, heads, ehs):
         B, N, _ = h.shape
         n1 = Fn.layer_norm(h, self.R(p + ".norm1.weight"), self.R(p + ".norm1.bias"))
         wqkv = self.R([p + ".attn1.to_q.weight", p + ".attn1.to_k.weight", p + ".attn1.to_v.weight"], (3 * C, C))
-        qkv = Fn.linear(n1, wqkv)
+        qkv = Fn.linear(n1, wqkv, lora=self._lo_fused([p + ".attn1.to_q", p + ".attn1.to_k", p + ".attn1.to_v"]))
         o = Fn.SelfAttnFn.apply(qkv, heads)
         h = self._linear(o, p + ".attn1.to_out.0", residual=h)
         n2 = Fn.layer_norm(h, self.R(p + ".norm2.weight"), self.R(p + ".norm2.bias"))
-        q = Fn.linear(n2, self.R(p + ".attn2.to_q.weight"))
+        q = Fn.linear(n2, self.R(p + ".attn2.to_q.weight"), lora=self._lo(p + ".attn2.to_q"))
         ctxd = self.cfg.cross_attention_dim
         wkv = self.R([p + ".attn2.to_k.weight", p + ".attn2.to_v.weight"], (2 * C, ctxd))
-        kv = Fn.linear(ehs, wkv)
+        kv = Fn.linear(ehs, wkv, lora=self._lo_fused([p + ".attn2.to_k", p + ".attn2.to_v"]))
         o = Fn.CrossAttnFn.apply(q, kv, heads)
         h = self._linear(o, p + ".attn2.to_out.0", residual=h)
         n3 = Fn.layer_norm(h, self.R(p + ".norm3.weight"), self.R(p + ".norm3.bias"))
@@ -342,7 +361,7 @@ class UNet2DConditionModel:
         semb = Fn.SiLUFn.apply(temb)
         ehs = encoder_hidden_states.to(BF16)
 
-        x = Fn.conv(sample, self.R("conv_in.weight"), self.R("conv_in.bias"))
+        x = self._conv(sample, "conv_in")
         skips = [x]
         nlev = len(cfg.block_out_channels)
         for i, bt in enumerate(cfg.down_block_types):
@@ -352,8 +371,7 @@ class UNet2DConditionModel:
                     x = self._transformer(x, f"down_blocks.{i}.attentions.{j}", cfg.transformer_layers_per_block[i], ehs)
                 skips.append(x)
             if i < nlev - 1:
-                p = f"down_blocks.{i}.downsamplers.0.conv"
-                x = Fn.conv(x, self.R(p + ".weight"), self.R(p + ".bias"), stride=2)
+                x = self._conv(x, f"down_blocks.{i}.downsamplers.0.conv", stride=2)
                 skips.append(x)
         x = self._resnet(x, "mid_block.resnets.0", semb)
         x = self._transformer(x, "mid_block.attentions.0", cfg.transformer_layers_per_block[-1], ehs)
@@ -366,10 +384,9 @@ class UNet2DConditionModel:
                 if bt.startswith("CrossAttn"):
                     x = self._transformer(x, f"up_blocks.{i}.attentions.{j}", rdepth[i], ehs)
             if i < nlev - 1:
-                p = f"up_blocks.{i}.upsamplers.0.conv"
-                x = Fn.conv(x, self.R(p + ".weight"), self.R(p + ".bias"), upsample=True)
+                x = self._conv(x, f"up_blocks.{i}.upsamplers.0.conv", upsample=True)
         h = self._gn(x, "conv_norm_out", True)
-        return Fn.conv(h, self.R("conv_out.weight"), self.R("conv_out.bias"))
+        return self._conv(h, "conv_out")
 
 
 def flops_per_image(cfg: UNetConfig, h: int, w: int, ctx_len: int = 77) -> float:

@@ -50,7 +50,7 @@ class GenericTrainer:
         self.model_setup.setup_train_device(self.model, cfg)
         self.parameters = self.model.parameters.parameters()
         if self.world > 1:
-            self.reducer = GradBucketReducer(self.model.unet.store, bucket_bytes=cfg.dp_bucket_mb << 20)
+            self.reducer = GradBucketReducer(self.model.train_store, bucket_bytes=cfg.dp_bucket_mb << 20)
         approx = self.data_loader.get_data_set().approximate_length() if self.data_loader is not None else 1
         self.lr_scheduler = create_lr_scheduler(self.model.optimizer, cfg.learning_rate_scheduler,
                                                 cfg.learning_rate_warmup_steps, cfg.learning_rate_cycles,
@@ -65,7 +65,7 @@ class GenericTrainer:
         """one micro-step; returns the (device) loss divided by GA, like GenericTrainer.py:692."""
         cfg, model, setup = self.config, self.model, self.model_setup
         tp = model.train_progress
-        store = model.unet.store
+        store = model.train_store
         out = setup.predict(model, batch, cfg, tp)
         loss = setup.calculate_loss(model, batch, out, cfg)
         loss = loss / cfg.gradient_accumulation_steps

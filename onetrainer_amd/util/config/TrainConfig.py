@@ -75,6 +75,10 @@ class TrainConfig:
     lora_alpha: float = 1.0
     lora_weight_dtype: str = "FLOAT_32"
     lora_layers: str = ""
+    lora_layer_preset: str | None = None
+    lora_decompose: bool = False
+    peft_type: str = "LORA"
+    dropout_probability: float = 0.0          # LoRA dropout (TrainConfig.py:828)
     # parts
     optimizer: OptimizerConfig = field(default_factory=OptimizerConfig)
     unet: ModelPartConfig = field(default_factory=ModelPartConfig)

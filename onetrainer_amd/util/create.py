@@ -13,7 +13,8 @@ SCALING = {"STABLE_DIFFUSION_XL_10_BASE": 0.13025, "STABLE_DIFFUSION_15": 0.1821
 
 
 def create_model(config, device, seed=0, unet_config=None, prediction_type="epsilon"):
-    """random-weight model of the configured architecture (weights from disk: SURVEY.md §8(f) #2)."""
+    """random-weight model of the configured architecture (weights from disk: SURVEY.md §8(f) #2).
+    LoRA training keeps the base UNet frozen (no gradient buffer)."""
     mt = config.model_type
     if unet_config is None:
         if mt.startswith("STABLE_DIFFUSION_XL"):
@@ -22,7 +23,7 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
             unet_config = U.sd15_config()
         else:
             raise NotImplementedError(f"model type {mt}")
-    unet = U.UNet2DConditionModel(unet_config, device, seed=seed)
+    unet = U.UNet2DConditionModel(unet_config, device, seed=seed, trainable=config.training_method != "LORA")
     ns = NoiseScheduler(device, prediction_type=prediction_type)
     return StableDiffusionXLModel(unet, ns, SCALING.get(mt, 0.13025), model_type=mt)
 
@@ -31,4 +32,7 @@ def create_model_setup(config, train_device, dp_rank=0, dp_world=1):
     if config.training_method == "FINE_TUNE":
         from ..modelSetup.StableDiffusionXLFineTuneSetup import StableDiffusionXLFineTuneSetup
         return StableDiffusionXLFineTuneSetup(train_device, dp_rank=dp_rank, dp_world=dp_world)
+    if config.training_method == "LORA":
+        from ..modelSetup.StableDiffusionXLLoRASetup import StableDiffusionXLLoRASetup
+        return StableDiffusionXLLoRASetup(train_device, dp_rank=dp_rank, dp_world=dp_world)
     raise NotImplementedError(f"training method {config.training_method}")
