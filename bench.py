@@ -34,7 +34,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(res=512, steps=1):
+def cpu_baseline(res=512, steps=1, sd15=False):
     """Oracle (CPU fp32 restatement of the reference step: diffusers UNet + DDPM noise + MSE +
     clip + torch AdamW) timed on this host's cores, SDXL at `res`^2, batch 1."""
     from oracle import unet as OU
@@ -42,7 +42,7 @@ def cpu_baseline(res=512, steps=1):
     threads = len(os.sched_getaffinity(0))
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     torch.set_num_threads(threads)
-    cfg = OU.sdxl_config()
+    cfg = OU.sd15_config() if sd15 else OU.sdxl_config()
     torch.manual_seed(0)
     t0 = time.time()
     with torch.device("meta"):
@@ -55,9 +55,9 @@ def cpu_baseline(res=512, steps=1):
     betas = OD.scaled_linear_betas()
     h = res // 8
     x0 = torch.randn(1, 4, h, h)
-    ehs = torch.randn(1, 77, 2048)
-    te = torch.randn(1, 1280)
-    tid = torch.tensor([[float(res), float(res), 0., 0., float(res), float(res)]])
+    ehs = torch.randn(1, 77, cfg.cross_attention_dim)
+    te = None if sd15 else torch.randn(1, 1280)
+    tid = None if sd15 else torch.tensor([[float(res), float(res), 0., 0., float(res), float(res)]])
     build_s = time.time() - t0
 
     def step(i):
@@ -111,18 +111,28 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=4, help="per-GPU batch")
-    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 4 sdxl / 16 sd15)")
+    ap.add_argument("--res", type=int, default=None, help="default 1024 (sdxl) / 512 (sd15)")
+    ap.add_argument("--model", choices=["sdxl", "sd15"], default="sdxl",
+                    help="sdxl: configs[2] per GPU (metric workload); sd15: configs[1] (SD 1.5 512^2 b=16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-res", type=int, default=512)
     args = ap.parse_args()
 
     from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_sdxl_batch
-    from onetrainer_amd.module.unet import flops_per_image, sdxl_config
+    from onetrainer_amd.module.unet import flops_per_image, sd15_config, sdxl_config
     from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
     from onetrainer_amd.util.config.TrainConfig import TrainConfig
 
+    sd15 = args.model == "sd15"
+    if args.res is None:
+        args.res = 512 if sd15 else 1024
+    if args.batch is None:
+        args.batch = 16 if sd15 else 4
+    ucfg = sd15_config() if sd15 else sdxl_config()
     cfg = TrainConfig.default_values()
+    if sd15:
+        cfg.model_type = "STABLE_DIFFUSION_15"
     cfg.batch_size = args.batch
     cfg.learning_rate = 3e-6
     cfg.learning_rate_warmup_steps = 0
@@ -135,7 +145,8 @@ def main():
     dev = tr.device
     log(f"[bench] rank {rank}/{world} model ready in {time.time() - t0:.1f}s "
         f"({tr.model.unet.num_parameters() / 1e9:.3f} B params)")
-    batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=rank)
+    batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=rank, sdxl=not sd15,
+                                 scaling_factor=0.18215 if sd15 else 0.13025)
 
     for i in range(args.warmup):
         tr.train_step(batch)
@@ -179,11 +190,12 @@ def main():
     imgs = args.batch * world * args.steps
     value = imgs / elapsed
     ms = 1000.0 * elapsed / args.steps
-    fwd_tf = flops_per_image(sdxl_config(), args.res // 8, args.res // 8) / 1e12
+    fwd_tf = flops_per_image(ucfg, args.res // 8, args.res // 8) / 1e12
     train_tf_img = 3.0 * fwd_tf                       # fwd + dgrad + wgrad
     achieved = train_tf_img * args.batch / (ms / 1000.0)   # per GPU, TFLOP/s
+    mname = "SD 1.5 UNet (859.5M params)" if sd15 else "SDXL 1.0 UNet (2.567B params)"
     out = {
-        "metric": "train images/sec (whole node) + step-time p50, SDXL 1024^2 bf16",
+        "metric": "train images/sec (whole node) + step-time p50, " + ("SD1.5 512^2 bf16" if sd15 else "SDXL 1024^2 bf16"),
         "value": round(value, 3),
         "unit": "images/s",
         "n_gpus": world,
@@ -197,9 +209,9 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random cached latents/text states, random-init weights)",
-        "config": {"workload": f"SDXL 1.0 UNet full fine-tune train step {args.res}^2 (latent {args.res // 8}^2), "
-                               f"b={args.batch}/GPU, AdamW+bf16 SR, clip 1.0",
-                   "model": "SDXL 1.0 UNet (2.567B params)", "global_batch": args.batch * world,
+        "config": {"workload": f"{'SD 1.5' if sd15 else 'SDXL 1.0'} UNet full fine-tune train step {args.res}^2 "
+                               f"(latent {args.res // 8}^2), b={args.batch}/GPU, AdamW+bf16 SR, clip 1.0",
+                   "model": mname, "global_batch": args.batch * world,
                    "seq_len": (args.res // 8) ** 2, "parallelism": f"dp{world}"},
         "loss": round(loss_val, 5),
         "roofline": {"bound": "mfma", "achieved": round(g_achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -217,12 +229,12 @@ def main():
         torch.cuda.empty_cache()
         log("[bench] cpu baseline (oracle, fp32) ...")
         try:
-            dt, threads, build_s = cpu_baseline(args.cpu_res, 1)
-            cpu_tf = 3.0 * flops_per_image(sdxl_config(), args.cpu_res // 8, args.cpu_res // 8) / 1e12
+            dt, threads, build_s = cpu_baseline(args.cpu_res, 1, sd15)
+            cpu_tf = 3.0 * flops_per_image(ucfg, args.cpu_res // 8, args.cpu_res // 8) / 1e12
             eq = (1.0 / dt) * cpu_tf / train_tf_img        # images/s at the bench resolution, by FLOP ratio
             out["cpu_baseline"] = {"value": round(eq, 5), "unit": "images/s", "cores": threads, "kind": "port",
                                    "sample": f"1 step of the oracle (CPU fp32 restatement: UNet fwd+bwd, DDPM noise, "
-                                             f"MSE, clip, torch AdamW) at SDXL {args.cpu_res}^2 b=1 took {dt:.2f}s; "
+                                             f"MSE, clip, torch AdamW) at {args.model} {args.cpu_res}^2 b=1 took {dt:.2f}s; "
                                              f"value scaled to {args.res}^2 by the FLOP ratio "
                                              f"({cpu_tf:.2f}/{train_tf_img:.2f} TFLOP)"}
         except Exception as e:   # the baseline must not sink the GPU measurement

@@ -50,6 +50,10 @@ typedef struct GemmArgs {
   const void* A2; long long lda2;
   const void* B2; long long ldb2;
   int K1, K2;
+  /* batched GEMM (K/MN modes, one segment, no split-K): grid.y = z < batch; operand bases move by
+     (z / bdiv) * s0 + (z % bdiv) * s1 elements ((image, head) pairs of [B, N, H*D] activations) */
+  int batch, bdiv;
+  long long sa0, sa1, sb0, sb1, sc0, sc1;
 } GemmArgs;
 
 typedef struct AttnArgs {
@@ -95,6 +99,15 @@ long long otamd_attn_bwd_ws_bytes(const AttnArgs* in);
 
 /* replaces: ABI check */
 int otamd_attn_args_size(void);
+
+/* replaces: the softmax inside F.scaled_dot_product_attention for heads wider than 128 (SD 1.5 160-wide heads,
+   v1-inference.yaml:29-44; VAE mid-block 512-wide head): P = softmax(scale S) row-wise, bf16 P, natural-log lse */
+int otamd_softmax_rows_fwd(const float* S, long long lds, void* P, long long ldp, float* lse, long long rows,
+                           int ncols, int ncols_pad, float scale, hipStream_t stream);
+
+/* replaces: autograd of that softmax: dS = scale P (dP - rowsum(P dP)) */
+int otamd_softmax_rows_bwd(const void* P, long long ldp, const float* dP, long long lddp, void* dS, long long ldds,
+                           long long rows, int ncols, int ncols_pad, float scale, hipStream_t stream);
 
 /* replaces: ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out (diffusers, via BaseStableDiffusionXLSetup.py:268-273) */
 int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long long ldy, int N, int HW, int C, int G,

@@ -31,7 +31,9 @@ class GemmArgs(C.Structure):
                 ("residual", C.c_void_p), ("ldr", C.c_longlong), ("slab", C.c_void_p), ("k_per_split", C.c_int),
                 ("ga", ConvGeom), ("gb", ConvGeom),
                 ("A2", C.c_void_p), ("lda2", C.c_longlong), ("B2", C.c_void_p), ("ldb2", C.c_longlong),
-                ("K1", C.c_int), ("K2", C.c_int)]
+                ("K1", C.c_int), ("K2", C.c_int),
+                ("batch", C.c_int), ("bdiv", C.c_int), ("sa0", C.c_longlong), ("sa1", C.c_longlong),
+                ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong)]
 
 
 class AdamwGroup(C.Structure):
@@ -85,6 +87,9 @@ SIGNATURES: dict[str, list] = {
     "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],
     "otamd_attn_bwd": [C.POINTER(AttnArgs), VP, LL, VP],
     "otamd_attn_bwd_ws_bytes": [C.POINTER(AttnArgs)],
+    # softmax.hip (materialized attention for heads > 128)
+    "otamd_softmax_rows_fwd": [VP, LL, VP, LL, VP, LL, I, I, F, VP],
+    "otamd_softmax_rows_bwd": [VP, LL, VP, LL, VP, LL, LL, I, I, F, VP],
     # elementwise.hip
     "otamd_geglu_fwd": [VP, LL, VP, LL, I, I, VP],
     "otamd_geglu_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP],

@@ -35,7 +35,22 @@ struct GemmArgs {
   const bf16_t* A2; long long lda2;
   const bf16_t* B2; long long ldb2;
   int K1, K2;
+  // batched GEMM (K/MN operand modes, one K segment, no split-K): grid.y = batch index z; every
+  // operand base moves by (z / bdiv) * s0 + (z % bdiv) * s1 elements -- (image, head) pairs of a
+  // [B, N, H*D] activation are bdiv = H, s0 = batch stride, s1 = D.  batch <= 1: unbatched.
+  int batch, bdiv;
+  long long sa0, sa1, sb0, sb1, sc0, sc1;
 };
+
+__device__ __forceinline__ void gemm_batch_offset(GemmArgs& a) {
+  if (a.batch > 1) {
+    const int z = blockIdx.y;
+    const long long q = z / a.bdiv, r = z - q * a.bdiv;
+    a.A += q * a.sa0 + r * a.sa1;
+    a.B += q * a.sb0 + r * a.sb1;
+    a.C = (char*)a.C + (q * a.sc0 + r * a.sc1) * (a.c_f32 ? 4 : 2);
+  }
+}
 
 
 __device__ __forceinline__ void add_bf8(float (&v)[8], const uint4& b) {

@@ -191,6 +191,7 @@ template <int MODE> struct IsK { static constexpr bool v = (MODE == OPM_K || MOD
 template <int AM, int BMODE>
 __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs args) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (AM <= OPM_MN && BMODE <= OPM_MN) gemm_batch_offset(args);
   const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -377,6 +378,7 @@ static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = fa
 OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out) {
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -1;
   int s = splits;
+  if (in->batch > 1) s = 1;
   if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT || in->A2 != nullptr).splits;
   if (splits_out) *splits_out = s;
   return s > 1 ? (long long)s * in->M * in->N * 4 : 0;
@@ -426,6 +428,13 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
       return OTAMD_EUNSUPPORTED;
     if ((a.lda2 % 8) || (a.ldb2 % 8) || (a.K2 % 8) || !aligned16(a.A2) || !aligned16(a.B2)) return OTAMD_EINVAL;
   }
+  if (a.batch > 1) {   // batched: plain K/MN operands, one segment, no split-K, no fused epilogue operands
+    if (a.bdiv <= 0 || a.batch > 65535 || a.A2 || a.amode > OPM_MN || a.bmode > OPM_MN || a.bias || a.rowvec ||
+        a.residual || splits > 1)
+      return OTAMD_EINVAL;
+    if ((a.sa0 | a.sa1 | a.sb0 | a.sb1) % 8 || (a.sc0 | a.sc1) % 4) return OTAMD_EINVAL;
+    splits = 1;
+  }
   GemmPlan plan = plan_gemm(a.M, a.N, a.K, splits > 0 ? splits : 32, v2_only);
   if (splits > 0) plan = plan_gemm(a.M, a.N, a.K, 1, v2_only), plan.splits = splits;
   splits = plan.splits;
@@ -457,7 +466,7 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
   if (rc != OTAMD_OK) {
     if (!fn || a.A2) return rc;   // v1 has no conv-weight B and no second K segment
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    dim3 grid(tiles, 1, splits);
+    dim3 grid(tiles, a.batch > 1 ? a.batch : 1, splits);
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);
     OTAMD_CHECK_LAUNCH();
   }

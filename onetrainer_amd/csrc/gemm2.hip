@@ -205,6 +205,7 @@ __global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, u
   constexpr int STAGE = ABYTES + BBYTES;
   constexpr int LOADS = Stage<AM, BM, NW>::NI + Stage<BMODE, BN, NW>::NI;
   constexpr bool AK = IsKMode<AM>::v, BKm = IsKMode<BMODE>::v;
+  if constexpr (!SEG2 && AM <= OPM_MN && BMODE <= OPM_MN) gemm_batch_offset(args);
 
   const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
@@ -424,7 +425,8 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   static bool attr_set[3] = {false, false, false};
   (void)attr_set;
   hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(fn, dim3(tiles, 1, splits), dim3(NWv * 64), lds, stream, a, (unsigned)ab, (unsigned)bb, a2b, b2b);
+  hipLaunchKernelGGL(fn, dim3(tiles, a.batch > 1 ? a.batch : 1, splits), dim3(NWv * 64), lds, stream, a, (unsigned)ab,
+                     (unsigned)bb, a2b, b2b);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

@@ -30,6 +30,8 @@ def synthetic_sdxl_batch(batch_size, height, width, device, seed=0, latent_dtype
         b["original_resolution"] = (hw(height), hw(width))
         b["crop_offset"] = (hw(0), hw(0))
         b["crop_resolution"] = (hw(height), hw(width))
+    else:   # SD 1.5 output names (StableDiffusionBaseDataLoader): one text encoder
+        b["text_encoder_hidden_state"] = b.pop("text_encoder_1_hidden_state")
     return b
 
 

@@ -424,8 +424,126 @@ def _attn_args(q, k, v, heads, scale):
     return a
 
 
+FLASH_MAX_D = 128
+
+
+def _span_ok(t: torch.Tensor, last_elem: int) -> bool:
+    """element offset `last_elem` (relative to t's first element) lies inside t's storage."""
+    return t.storage_offset() + last_elem < t.untyped_storage().nbytes() // t.element_size()
+
+
+def gemm_batched(A, lda, amode, B, ldb, bmode, Cm, ldc, M, N, K, batch, bdiv, sa, sb, sc, alpha=1.0,
+                 accumulate=False):
+    """C_z[M,N] = alpha A_z B_z for z < batch; operand bases at (z // bdiv) * s[0] + (z % bdiv) * s[1]
+    elements from A / B / C's first element.  K-mode A: A_z[m][k] at m*lda + k; MN-mode A at
+    k*lda + m (likewise B with n).  Bounds of the last batch element are checked on the host."""
+    _req(A.dtype == BF16 and B.dtype == BF16 and Cm.dtype in (BF16, F32), "batched gemm dtypes")
+    _req(_aligned(A) and _aligned(B) and _aligned(Cm), "batched gemm: 16-byte aligned operands")
+    last = lambda s_: ((batch - 1) // bdiv) * s_[0] + (min(bdiv, batch) - 1) * s_[1]   # noqa: E731
+    ext_a = (M - 1) * lda + K if amode == OPM_K else (K - 1) * lda + M
+    ext_b = (N - 1) * ldb + K if bmode == OPM_K else (K - 1) * ldb + N
+    _req(_span_ok(A, last(sa) + ext_a - 1) and _span_ok(B, last(sb) + ext_b - 1)
+         and _span_ok(Cm, last(sc) + (M - 1) * ldc + N - 1), "batched gemm operand out of bounds")
+    a = _new_args()
+    a.A, a.lda, a.amode = _p(A), lda, amode
+    a.B, a.ldb, a.bmode = _p(B), ldb, bmode
+    a.C, a.ldc, a.c_f32, a.accumulate = _p(Cm), ldc, int(Cm.dtype == F32), int(accumulate)
+    a.M, a.N, a.K, a.alpha = M, N, K, alpha
+    a.batch, a.bdiv = batch, bdiv
+    a.sa0, a.sa1 = sa
+    a.sb0, a.sb1 = sb
+    a.sc0, a.sc1 = sc
+    _gemm(a, 1, A.device)
+
+
+def softmax_rows_fwd(S, P, lse, ncols, scale):
+    """P[r, :ncols] = softmax(scale * S[r, :ncols]) (bf16), P[r, ncols:] = 0; lse natural log."""
+    rows = S.numel() // S.shape[-1]
+    _req(S.dtype == F32 and P.dtype == BF16 and S.is_contiguous() and P.is_contiguous(), "softmax operands")
+    _req(P.numel() // P.shape[-1] == rows and lse.numel() == rows and lse.dtype == F32, "softmax shapes")
+    check(lib().otamd_softmax_rows_fwd(_p(S), S.shape[-1], _p(P), P.shape[-1], _p(lse), rows, ncols, P.shape[-1],
+                                       float(scale), stream_handle()), "otamd_softmax_rows_fwd")
+
+
+def softmax_rows_bwd(P, dP, dS, ncols, scale):
+    rows = P.numel() // P.shape[-1]
+    _req(P.dtype == BF16 and dP.dtype == F32 and dS.dtype == BF16 and P.is_contiguous() and dP.is_contiguous()
+         and dS.is_contiguous() and dP.numel() // dP.shape[-1] == rows and dS.shape == P.shape, "softmax bwd operands")
+    check(lib().otamd_softmax_rows_bwd(_p(P), P.shape[-1], _p(dP), dP.shape[-1], _p(dS), dS.shape[-1], rows, ncols,
+                                       dS.shape[-1], float(scale), stream_handle()), "otamd_softmax_rows_bwd")
+
+
+def _pad_keys(t: torch.Tensor, nkp: int) -> torch.Tensor:
+    if t.shape[1] == nkp:
+        return t
+    out = torch.zeros((t.shape[0], nkp, t.shape[2]), dtype=t.dtype, device=t.device)
+    out[:, :t.shape[1]].copy_(t)
+    return out
+
+
+def _mat_geom(q, k, heads):
+    B, Nq, Cq = q.shape
+    Nk = k.shape[1]
+    D = Cq // heads
+    _req(D % 8 == 0, "head dim must be a multiple of 8")
+    return B, Nq, Nk, (Nk + 7) // 8 * 8, D
+
+
+def attn_mat_fwd(q, k, v, heads, scale=None, out=None):
+    """Materialized attention (heads wider than the flash kernels): S = q k^T (fp32, batched
+    MFMA GEMM) -> P = softmax(scale S) -> o = P v.  Returns (o, P [B*H, Nq, Nk_pad] bf16)."""
+    B, Nq, Nk, Nkp, D = _mat_geom(q, k, heads)
+    H = heads
+    scale = scale if scale is not None else D ** -0.5
+    kp, vp = _pad_keys(k, Nkp), _pad_keys(v, Nkp)
+    S = torch.empty((B * H, Nq, Nkp), dtype=F32, device=q.device)
+    gemm_batched(q, q.stride(1), OPM_K, kp, kp.stride(1), OPM_K, S, Nkp, Nq, Nkp, D, B * H, H,
+                 (q.stride(0), D), (kp.stride(0), D), (H * Nq * Nkp, Nq * Nkp))
+    P = torch.empty((B * H, Nq, Nkp), dtype=BF16, device=q.device)
+    lse = torch.empty((B * H, Nq), dtype=F32, device=q.device)
+    softmax_rows_fwd(S, P, lse, Nk, scale)
+    del S
+    if out is None:
+        out = torch.empty(q.shape, dtype=BF16, device=q.device)
+    gemm_batched(P, Nkp, OPM_K, vp, vp.stride(1), OPM_MN, out, out.stride(1), Nq, D, Nkp, B * H, H,
+                 (H * Nq * Nkp, Nq * Nkp), (vp.stride(0), D), (out.stride(0), D))
+    return out, P
+
+
+def attn_mat_bwd(q, k, v, P, dout, heads, scale=None, dq=None, dk=None, dv=None):
+    B, Nq, Nk, Nkp, D = _mat_geom(q, k, heads)
+    H = heads
+    scale = scale if scale is not None else D ** -0.5
+    kp, vp = _pad_keys(k, Nkp), _pad_keys(v, Nkp)
+    dq = torch.empty(q.shape, dtype=BF16, device=q.device) if dq is None else dq
+    dk = torch.empty(k.shape, dtype=BF16, device=q.device) if dk is None else dk
+    dv = torch.empty(v.shape, dtype=BF16, device=q.device) if dv is None else dv
+    zs = (H * Nq * Nkp, Nq * Nkp)
+    dP = torch.empty((B * H, Nq, Nkp), dtype=F32, device=q.device)
+    gemm_batched(dout, dout.stride(1), OPM_K, vp, vp.stride(1), OPM_K, dP, Nkp, Nq, Nkp, D, B * H, H,
+                 (dout.stride(0), D), (vp.stride(0), D), zs)
+    dS = torch.empty((B * H, Nq, Nkp), dtype=BF16, device=q.device)
+    softmax_rows_bwd(P, dP, dS, Nk, scale)
+    del dP
+    gemm_batched(dS, Nkp, OPM_K, kp, kp.stride(1), OPM_MN, dq, dq.stride(1), Nq, D, Nkp, B * H, H,
+                 zs, (kp.stride(0), D), (dq.stride(0), D))
+    dkp = dk if Nkp == Nk else torch.empty((B, Nkp, k.shape[2]), dtype=BF16, device=q.device)
+    dvp = dv if Nkp == Nk else torch.empty((B, Nkp, v.shape[2]), dtype=BF16, device=q.device)
+    gemm_batched(dS, Nkp, OPM_MN, q, q.stride(1), OPM_MN, dkp, dkp.stride(1), Nkp, D, Nq, B * H, H,
+                 zs, (q.stride(0), D), (dkp.stride(0), D))
+    gemm_batched(P, Nkp, OPM_MN, dout, dout.stride(1), OPM_MN, dvp, dvp.stride(1), Nkp, D, Nq, B * H, H,
+                 zs, (dout.stride(0), D), (dvp.stride(0), D))
+    if Nkp != Nk:
+        dk.copy_(dkp[:, :Nk])
+        dv.copy_(dvp[:, :Nk])
+    return dq, dk, dv
+
+
 def attn_fwd(q, k, v, heads, scale=None, out=None):
-    """softmax(q k^T * scale) v per head; returns (o [B,Nq,H*D] bf16, lse [B,H,Nq] f32 log2-domain)."""
+    """softmax(q k^T * scale) v per head; returns (o [B,Nq,H*D] bf16, aux): aux is the flash
+    kernels' lse [B,H,Nq] (log2 domain) for head dims <= 128, else the materialized P."""
+    if q.shape[-1] // heads > FLASH_MAX_D:
+        return attn_mat_fwd(q, k, v, heads, scale, out)
     a = _attn_args(q, k, v, heads, scale)
     if out is None:
         out = torch.empty(q.shape, dtype=BF16, device=q.device)
@@ -437,6 +555,8 @@ def attn_fwd(q, k, v, heads, scale=None, out=None):
 
 
 def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None):
+    if q.shape[-1] // heads > FLASH_MAX_D:
+        return attn_mat_bwd(q, k, v, lse, dout, heads, scale, dq, dk, dv)
     a = _attn_args(q, k, v, heads, scale)
     dq = torch.empty(q.shape, dtype=BF16, device=q.device) if dq is None else dq
     dk = torch.empty(k.shape, dtype=BF16, device=q.device) if dk is None else dk

@@ -77,6 +77,15 @@ def tiny_sdxl_config() -> UNetConfig:
                       projection_class_embeddings_input_dim=64 + 6 * 32, norm_num_groups=32)
 
 
+def tiny_sd15_config() -> UNetConfig:
+    """SD 1.5-shaped (conv proj_in/out, no add-embedding, fixed head count) at test size; 2 heads
+    give 80-wide heads (flash kernels) and 160-wide heads (materialized path) like SD 1.5's."""
+    return UNetConfig(block_out_channels=(160, 320), down_block_types=("CrossAttnDownBlock2D", "DownBlock2D"),
+                      up_block_types=("UpBlock2D", "CrossAttnUpBlock2D"), transformer_layers_per_block=(1, 1),
+                      head_dim=None, num_heads=2, cross_attention_dim=96, use_linear_projection=False,
+                      addition_embed=False, norm_num_groups=32)
+
+
 PAD_IN = 8    # conv_in input channels held (latent channels zero-padded)
 PAD_OUT = 8   # conv_out output channels held
 

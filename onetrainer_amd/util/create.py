@@ -19,7 +19,7 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
     if unet_config is None:
         if mt.startswith("STABLE_DIFFUSION_XL"):
             unet_config = U.sdxl_config()
-        elif mt.startswith("STABLE_DIFFUSION_15") or mt == "STABLE_DIFFUSION_15":
+        elif is_sd15(mt):
             unet_config = U.sd15_config()
         else:
             raise NotImplementedError(f"model type {mt}")
@@ -28,11 +28,25 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
     return StableDiffusionXLModel(unet, ns, SCALING.get(mt, 0.13025), model_type=mt)
 
 
+def is_sd15(model_type: str) -> bool:
+    return model_type.startswith("STABLE_DIFFUSION_15") or model_type in ("STABLE_DIFFUSION_15_INPAINTING",)
+
+
 def create_model_setup(config, train_device, dp_rank=0, dp_world=1):
+    """ModelType x TrainingMethod -> plugin (create.py:285-353)."""
+    sd15 = is_sd15(config.model_type)
+    if not sd15 and not config.model_type.startswith("STABLE_DIFFUSION_XL"):
+        raise NotImplementedError(f"model type {config.model_type}")
     if config.training_method == "FINE_TUNE":
-        from ..modelSetup.StableDiffusionXLFineTuneSetup import StableDiffusionXLFineTuneSetup
-        return StableDiffusionXLFineTuneSetup(train_device, dp_rank=dp_rank, dp_world=dp_world)
+        if sd15:
+            from ..modelSetup.StableDiffusionFineTuneSetup import StableDiffusionFineTuneSetup as S
+        else:
+            from ..modelSetup.StableDiffusionXLFineTuneSetup import StableDiffusionXLFineTuneSetup as S
+        return S(train_device, dp_rank=dp_rank, dp_world=dp_world)
     if config.training_method == "LORA":
-        from ..modelSetup.StableDiffusionXLLoRASetup import StableDiffusionXLLoRASetup
-        return StableDiffusionXLLoRASetup(train_device, dp_rank=dp_rank, dp_world=dp_world)
+        if sd15:
+            from ..modelSetup.StableDiffusionLoRASetup import StableDiffusionLoRASetup as S
+        else:
+            from ..modelSetup.StableDiffusionXLLoRASetup import StableDiffusionXLLoRASetup as S
+        return S(train_device, dp_rank=dp_rank, dp_world=dp_world)
     raise NotImplementedError(f"training method {config.training_method}")

@@ -86,6 +86,46 @@ def test_attention(dev, B, Nq, Nk, H, D):
         assert rel_err(got, want.transpose(1, 2).reshape(got.shape)) < 3e-2
 
 
+@pytest.mark.parametrize("B,Nq,Nk,H,D,fused", [(2, 256, 256, 8, 160, True), (2, 256, 77, 8, 160, False),
+                                               (1, 1024, 1024, 1, 512, False), (3, 64, 64, 2, 160, True),
+                                               (2, 300, 77, 8, 80, False)])
+def test_attention_wide_heads(dev, B, Nq, Nk, H, D, fused):
+    """heads > 128 (SD 1.5 level-2 160-wide heads, VAE 512-wide single head): materialized path
+    (batched MFMA GEMMs + row softmax kernels); D = 80 stays on the flash kernels."""
+    torch.manual_seed(4)
+    C = H * D
+    if fused:
+        qkv = rnd(B, Nq, 3 * C, dev=dev)
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    else:
+        q, k, v = rnd(B, Nq, C, dev=dev), rnd(B, Nk, C, dev=dev), rnd(B, Nk, C, dev=dev)
+    o, aux = K.attn_fwd(q, k, v, H)
+    qh, kh, vh = sdpa_ref(q, k, v, H)
+    qh.requires_grad_(True); kh.requires_grad_(True); vh.requires_grad_(True)
+    ref = F.scaled_dot_product_attention(qh, kh, vh)
+    assert rel_err(o, ref.transpose(1, 2).reshape(B, Nq, C)) < 2e-2
+    do = rnd(B, Nq, C, dev=dev)
+    ref.backward(do.float().view(B, Nq, H, D).transpose(1, 2))
+    dq, dk, dv = K.attn_bwd(q, k, v, o, aux, do, H)
+    for got, want in ((dq, qh.grad), (dk, kh.grad), (dv, vh.grad)):
+        assert rel_err(got, want.transpose(1, 2).reshape(got.shape)) < 3e-2
+
+
+def test_gemm_batched_heads(dev):
+    # C_z = A_z B_z^T over (image, head) pairs of [B, N, H*D] operands, fp32 out
+    torch.manual_seed(5)
+    B, H, M, N, D = 3, 4, 136, 96, 48
+    a, b = rnd(B, M, H * D, dev=dev), rnd(B, N, H * D, dev=dev)
+    c = torch.empty(B * H, M, N, device=dev)
+    K.gemm_batched(a, H * D, K.OPM_K, b, H * D, K.OPM_K, c, N, M, N, D, B * H, H, (M * H * D, D), (N * H * D, D),
+                   (H * M * N, M * N))
+    ref = torch.einsum("bmhd,bnhd->bhmn", a.float().view(B, M, H, D), b.float().view(B, N, H, D)).reshape(B * H, M, N)
+    assert rel_err(c, ref) < 1e-2
+    with pytest.raises(ValueError, match="out of bounds"):
+        K.gemm_batched(a, H * D, K.OPM_K, b, H * D, K.OPM_K, c, N, M, N, D, B * H + 1, H, (M * H * D, D),
+                       (N * H * D, D), (H * M * N, M * N))
+
+
 def test_attention_strided_qkv(dev):
     # q/k/v as column slices of one fused projection output (token stride 3*C)
     torch.manual_seed(3)

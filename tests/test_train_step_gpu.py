@@ -67,6 +67,51 @@ def test_train_step_matches_oracle(dev, ptype):
         assert abs(a - b) <= 2e-2 * abs(b), (ours, ref)
 
 
+def test_sd15_train_step_matches_oracle(dev):
+    """SD 1.5 plugin (BaseStableDiffusionSetup.py:135-330): one text encoder, no add-embedding,
+    80-wide (flash) and 160-wide (materialized) heads."""
+    torch.manual_seed(0)
+    ucfg = U.tiny_sd15_config()
+    cfg = TrainConfig.default_values()
+    cfg.model_type = "STABLE_DIFFUSION_15"
+    cfg.batch_size = 2
+    cfg.learning_rate = 1e-4
+    cfg.learning_rate_warmup_steps = 0
+    cfg.optimizer.stochastic_rounding = False
+    model = create.create_model(cfg, dev, seed=3, unet_config=ucfg)
+    assert model.vae.config["scaling_factor"] == 0.18215
+    om = OU.UNet2DConditionModel(_oracle_cfg(ucfg))
+    om.load_state_dict({k: v.float().cpu() for k, v in model.unet.state_dict().items()})
+    tr = GenericTrainer(cfg, model=model)
+    tr.start()
+    assert type(tr.model_setup).__name__ == "StableDiffusionFineTuneSetup"
+    res = 128
+    batch = synthetic_sdxl_batch(2, res, res, dev, seed=1, te1_dim=96, sdxl=False, scaling_factor=0.18215)
+    opt = torch.optim.AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2, foreach=False)
+    betas = OD.scaled_linear_betas()
+    lat = batch["latent_image"].cpu().permute(0, 3, 1, 2).float()
+    ehs = batch["text_encoder_hidden_state"].float().cpu()
+    ours, ref = [], []
+    for step in range(2):
+        gs = model.train_progress.global_step
+        noise = K.noise((2, res // 8, res // 8, 4), seed=gs, dtype=torch.float32, device=dev)
+        t = K.timesteps(2, seed=gs, device=dev)
+        ours.append(tr.train_step(batch).item())
+        eps = noise.cpu().permute(0, 3, 1, 2)
+        tc = t.cpu().long()
+        xt = OD.add_noise_ddpm(lat * 0.18215, eps, tc, betas)
+        pred = om(xt.bfloat16().float(), tc, ehs)
+        loss = OD.diffusion_losses(pred, eps, torch.ones(2)).mean()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(om.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad()
+        ref.append(loss.item())
+    print("sd15 losses hip", ours, "oracle", ref)
+    assert abs(ours[0] - ref[0]) <= 1e-3 * abs(ref[0]), (ours, ref)
+    assert abs(ours[1] - ref[1]) <= 2e-2 * abs(ref[1]), (ours, ref)
+
+
 def test_dp_noise_slices_match_global(dev):
     """rank r's predict() draws exactly samples [r*b, (r+1)*b) of the global batch's noise."""
     from onetrainer_amd.modelSetup.BaseStableDiffusionXLSetup import BaseStableDiffusionXLSetup

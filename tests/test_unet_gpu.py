@@ -17,10 +17,10 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
-@pytest.mark.parametrize("cfgname", ["tiny_sdxl"])
+@pytest.mark.parametrize("cfgname", ["tiny_sdxl", "tiny_sd15"])
 def test_unet_forward_backward_matches_oracle(dev, cfgname):
     torch.manual_seed(0)
-    cfg = U.tiny_sdxl_config()
+    cfg = getattr(U, cfgname + "_config")()
     m = U.UNet2DConditionModel(cfg, dev, seed=1)
     om = OU.UNet2DConditionModel(_oracle_cfg(cfg))
     om.load_state_dict({k: v.float().cpu() for k, v in m.state_dict().items()})
@@ -30,11 +30,14 @@ def test_unet_forward_backward_matches_oracle(dev, cfgname):
     ehs = torch.randn(B, 77, cfg.cross_attention_dim)
     te = torch.randn(B, cfg.projection_class_embeddings_input_dim - 6 * cfg.addition_time_embed_dim)
     tid = torch.tensor([[128., 128., 0., 0., 128., 128.]] * B)
+    if not cfg.addition_embed:   # SD 1.5: no pooled text / time_ids conditioning
+        te = tid = None
     xin = torch.zeros(B, H, W, 8, dtype=torch.bfloat16, device=dev)
     xin[..., :4] = x.permute(0, 2, 3, 1).to(dev).bfloat16()
-    out = m(xin, t.to(dev), ehs.to(dev).bfloat16(), te.to(dev).bfloat16(), tid.to(dev))
+    dv = (lambda v: None if v is None else v.to(dev))
+    out = m(xin, t.to(dev), ehs.to(dev).bfloat16(), None if te is None else te.to(dev).bfloat16(), dv(tid))
     # oracle sees the same bf16-rounded inputs
-    ref = om(x.bfloat16().float(), t, ehs.bfloat16().float(), te.bfloat16().float(), tid)
+    ref = om(x.bfloat16().float(), t, ehs.bfloat16().float(), None if te is None else te.bfloat16().float(), tid)
     o4 = out[..., :4].float().cpu()
     r4 = ref.permute(0, 2, 3, 1)
     err = (o4 - r4.detach()).abs().max() / r4.detach().abs().max()
