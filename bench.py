@@ -116,6 +116,7 @@ def main():
     ap.add_argument("--model", choices=["sdxl", "sd15"], default="sdxl",
                     help="sdxl: configs[2] per GPU (metric workload); sd15: configs[1] (SD 1.5 512^2 b=16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-vae", action="store_true", help="skip the VAE-encode (latent caching) side measurement")
     ap.add_argument("--cpu-res", type=int, default=512)
     args = ap.parse_args()
 
@@ -185,6 +186,10 @@ def main():
         raise RuntimeError(f"non-finite loss {loss_val}")
 
     g_flops, g_ms, g_n = gemm_roofline(tr, batch)
+    vae = None
+    if not args.no_vae:   # latent caching, reported beside the step, not part of `value`
+        from tools.bench_vae import run as vae_run
+        vae = vae_run(args.res, args.batch, iters=5, warmup=1, device=str(dev))
     g_achieved = g_flops / (g_ms * 1e-3) / 1e12
 
     imgs = args.batch * world * args.steps
@@ -223,6 +228,7 @@ def main():
                      "step_basis": f"{train_tf_img:.3f} TFLOP/image algorithmic (3 x {fwd_tf:.3f} fwd) x per-GPU "
                                    "images / step time"},
         "cpu_baseline": None,
+        "vae_encode": vae,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del tr

@@ -109,6 +109,11 @@ int otamd_softmax_rows_fwd(const float* S, long long lds, void* P, long long ldp
 int otamd_softmax_rows_bwd(const void* P, long long ldp, const float* dP, long long lddp, void* dS, long long ldds,
                            long long rows, int ncols, int ncols_pad, float scale, hipStream_t stream);
 
+/* replaces: mgds RescaleImageChannels(0..1 -> -1..1) + the NCHW image handed to AutoencoderKL.encode
+   (StableDiffusionXLBaseDataLoader.py:66-67): out[b,h,w,c] = img[b,c,h,w] * mul + add, NHWC bf16, c >= C zero */
+int otamd_image_to_nhwc(const float* img, int B, int C, int H, int W, float mul, float add, void* out, int cpad,
+                        hipStream_t s);
+
 /* replaces: ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out (diffusers, via BaseStableDiffusionXLSetup.py:268-273) */
 int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long long ldy, int N, int HW, int C, int G,
     float eps, const void* gamma, const void* beta, int silu, float* mean, float* rstd, float* a, float* b,

@@ -105,6 +105,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_lora_shadow_entry_size": [],
     "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
     "otamd_add": [VP, VP, VP, LL, VP],
+    "otamd_image_to_nhwc": [VP, I, I, I, I, F, F, VP, I, VP],
     # diffusion.hip
     "otamd_noise": [VP, I, LL, LL, U64, VP],
     "otamd_timesteps": [VP, I, LL, U64, I, I, F, F, F, F, F, VP],

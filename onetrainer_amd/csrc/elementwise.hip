@@ -355,3 +355,34 @@ OTAMD_API int otamd_add(const void* a, const void* b, void* y, long long n, hipS
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
+
+// Image batch -> VAE encoder input: mgds RescaleImageChannels (0..1 -> -1..1, i.e. x * mul + add;
+// StableDiffusionXLBaseDataLoader.py:66) fused with the NCHW fp32 -> NHWC bf16 relayout, channels
+// zero-padded to cpad (conv_in reads whole 16-byte chunks).  One thread per output pixel.
+__global__ void __launch_bounds__(256) image_to_nhwc_kernel(const float* __restrict__ img, int B, int C, int H, int W,
+                                                            float mul, float add, bf16_t* __restrict__ out,
+                                                            int cpad) {
+  const long long npix = (long long)B * H * W;
+  const long long hw = (long long)H * W;
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < npix; p += (long long)gridDim.x * blockDim.x) {
+    const long long b = p / hw, r = p - b * hw;
+    bf16_t* o = out + p * cpad;
+    for (int c0 = 0; c0 < cpad; c0 += 8) {
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        f[j] = c < C ? fmaf(img[(b * C + c) * hw + r], mul, add) : 0.f;
+      }
+      *reinterpret_cast<bf8*>(o + c0) = pack8(f);
+    }
+  }
+}
+
+OTAMD_API int otamd_image_to_nhwc(const float* img, int B, int C, int H, int W, float mul, float add, void* out,
+                                  int cpad, hipStream_t s) {
+  if (!img || !out || B <= 0 || C <= 0 || H <= 0 || W <= 0 || cpad < C || cpad % 8 || !al16(out)) return OTAMD_EINVAL;
+  image_to_nhwc_kernel<<<grid_for((long long)B * H * W), 256, 0, s>>>(img, B, C, H, W, mul, add, (bf16_t*)out, cpad);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}

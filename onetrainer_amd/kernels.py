@@ -207,14 +207,19 @@ def _nhwc(x: torch.Tensor):
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, pad=1, upsample=False, residual=None,
-           rowvec=None, out=None, lora=None) -> torch.Tensor:
+           rowvec=None, out=None, lora=None, out_hw=None) -> torch.Tensor:
     """NHWC conv: y[n,p,q,co] = sum w[co,r,s,ci] * x[n, p*st+r-pad, q*st+s-pad, ci] (+bias, +rowvec[n], +residual).
-    upsample=True reads x through a nearest-2x upsample (diffusers Upsample2D)."""
+    upsample=True reads x through a nearest-2x upsample (diffusers Upsample2D).  out_hw overrides the
+    output size: taps past the bottom / right edge read zeros, so pad=0 with out_hw = (H/2, W/2)
+    is the VAE Downsample2D's F.pad(x, (0, 1, 0, 1)) + stride-2 conv."""
     N, H, W, Cin, ldx = _nhwc(x)
     Cout, KH, KW, Cin2 = w.shape
     _req(Cin2 == Cin and w.dtype == BF16 and w.is_contiguous() and Cout % 8 == 0, "conv weight [Cout,KH,KW,Cin]")
     _req(_aligned(x) and _aligned(w), "aligned operands")
     P, Q = conv_out_hw(H, W, KH, stride, pad, upsample)
+    if out_hw is not None:
+        _req(not upsample and out_hw[0] <= P + 1 and out_hw[1] <= Q + 1 and min(out_hw) > 0, "conv out_hw")
+        P, Q = out_hw
     M = N * P * Q
     if out is None:
         out = torch.empty((N, P, Q, Cout), dtype=BF16, device=x.device)
@@ -687,6 +692,16 @@ def timestep_embedding(t_f32, dim, out=None):
         out = torch.empty((n, dim), dtype=BF16, device=t_f32.device)
     check(lib().otamd_timestep_embedding(_p(t_f32), n, dim, _p(out), out.stride(0), stream_handle()),
           "otamd_timestep_embedding")
+    return out
+
+
+def image_to_nhwc(img, mul=2.0, add_=-1.0, cpad=8):
+    """[B, C, H, W] fp32 image -> NHWC bf16 [B, H, W, cpad] with x * mul + add (0..1 -> -1..1)."""
+    _req(img.dim() == 4 and img.dtype == F32 and img.is_contiguous() and img.is_cuda, "image: contiguous fp32 NCHW")
+    B, C_, H, W = img.shape
+    out = torch.empty((B, H, W, cpad), dtype=BF16, device=img.device)
+    check(lib().otamd_image_to_nhwc(_p(img), B, C_, H, W, float(mul), float(add_), _p(out), cpad, stream_handle()),
+          "otamd_image_to_nhwc")
     return out
 
 

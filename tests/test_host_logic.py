@@ -92,3 +92,17 @@ def test_flop_counter_matches_survey():
     assert abs(U.flops_per_image(U.sdxl_config(), 128, 128) / 1e12 - 6.761) < 1e-3
     assert abs(U.flops_per_image(U.sdxl_config(), 64, 64) / 1e12 - 1.589) < 1e-3
     assert abs(U.flops_per_image(U.sd15_config(), 64, 64) / 1e12 - 0.803) < 1e-3
+
+
+def test_vae_encoder_spec_and_flops():
+    """VAE encoder 1.12 TF @512, 4.88 TF @1024; 34.16M params, names equal
+    to the oracle's (diffusers AutoencoderKL encoder + quant_conv)."""
+    from onetrainer_amd.module import vae as V
+    from oracle import vae as OV
+    cfg = V.sdxl_vae_config()
+    assert abs(V.flops_per_image(cfg, 1024, 1024) / 1e12 - 4.88) < 5e-3
+    assert abs(V.flops_per_image(cfg, 512, 512) / 1e12 - 1.12) < 5e-3
+    specs = V.vae_encoder_specs(cfg)
+    om = OV.AutoencoderKLEncoder(cfg)
+    assert {n for n, *_ in specs} == set(om.state_dict())
+    assert sum(math.prod(s) for _, s, _, _ in specs) == sum(p.numel() for p in om.parameters()) == 34_163_664

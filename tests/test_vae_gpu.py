@@ -1,0 +1,57 @@
+"""VAE-encode latent caching: HIP AutoencoderKL encoder (bf16, NHWC) vs the
+oracle (fp32 CPU restatement of diffusers AutoencoderKL.encode(...).latent_dist.mean), same
+weights and images.  Tolerance: bf16 activations with fp32 accumulation vs fp32 -> max abs error
+<= 3e-2 of the latent range, cosine >= 0.9995 (parity unpinned: diffusers is not in the image)."""
+import pytest
+import torch
+
+from onetrainer_amd import kernels as K
+from onetrainer_amd.module import vae as V
+from oracle import vae as OV
+
+pytestmark = pytest.mark.gpu
+
+
+def _cos(a, b):
+    a, b = a.flatten().double(), b.flatten().double()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("cfgname,B,H,W", [("tiny", 2, 64, 96), ("sdxl", 1, 256, 256)])
+def test_vae_encode_matches_oracle(dev, cfgname, B, H, W):
+    torch.manual_seed(0)
+    cfg = V.tiny_vae_config() if cfgname == "tiny" else V.sdxl_vae_config()
+    enc = V.AutoencoderKLEncoder(cfg, dev, seed=1)
+    om = OV.AutoencoderKLEncoder(cfg)
+    om.load_state_dict({k: v.float().cpu() for k, v in enc.state_dict().items()})
+    img = torch.rand(B, 3, H, W)
+    lat = enc.encode(img.to(dev))
+    assert lat.shape == (B, H // 2 ** (len(cfg.block_out_channels) - 1), W // 2 ** (len(cfg.block_out_channels) - 1),
+                         cfg.latent_channels) and lat.dtype == torch.float32
+    with torch.no_grad():
+        # the oracle sees the same bf16-rounded rescaled input
+        ref = om.quant_conv(om.encoder(((img * 2 - 1).bfloat16().float())))[:, :cfg.latent_channels]
+    ref = ref.permute(0, 2, 3, 1)
+    err = (lat.cpu() - ref).abs().max() / ref.abs().max()
+    assert err < 3e-2, f"rel err {err}"
+    assert _cos(lat.cpu(), ref) > 0.9995
+
+
+def test_image_to_nhwc(dev):
+    img = torch.rand(2, 3, 8, 16, device=dev)
+    x = K.image_to_nhwc(img)
+    assert x.shape == (2, 8, 16, 8)
+    ref = (img * 2 - 1).permute(0, 2, 3, 1).bfloat16()
+    assert torch.equal(x[..., :3], ref) and torch.count_nonzero(x[..., 3:]) == 0
+
+
+def test_downsample_conv_one_sided_padding(dev):
+    """F.pad(x, (0,1,0,1)) + 3x3 stride-2 conv == the conv gather with pad 0 and out_hw = H/2."""
+    torch.manual_seed(1)
+    x = torch.randn(2, 16, 24, 64, device=dev).bfloat16()
+    w = (torch.randn(64, 64, 3, 3, device=dev) * 0.05)
+    b = torch.randn(64, device=dev) * 0.1
+    y = K.conv2d(x, w.permute(0, 2, 3, 1).contiguous().bfloat16(), bias=b.bfloat16(), stride=2, pad=0, out_hw=(8, 12))
+    ref = torch.nn.functional.conv2d(torch.nn.functional.pad(x.permute(0, 3, 1, 2).float(), (0, 1, 0, 1)),
+                                     w.bfloat16().float(), b.bfloat16().float(), stride=2)
+    assert ((y.permute(0, 3, 1, 2).float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
