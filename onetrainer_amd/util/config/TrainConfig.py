@@ -43,6 +43,9 @@ class TrainConfig:
     weight_dtype: str = "BFLOAT_16"
     resolution: str = "1024"
     batch_size: int = 1
+    aspect_ratio_bucketing: bool = True       # TrainConfig.py:795
+    latent_caching: bool = True
+    cache_dir: str = "workspace-cache/run"
     gradient_accumulation_steps: int = 1
     epochs: int = 100
     learning_rate: float = 3e-6

@@ -55,3 +55,35 @@ def test_downsample_conv_one_sided_padding(dev):
     ref = torch.nn.functional.conv2d(torch.nn.functional.pad(x.permute(0, 3, 1, 2).float(), (0, 1, 0, 1)),
                                      w.bfloat16().float(), b.bfloat16().float(), stride=2)
     assert ((y.permute(0, 3, 1, 2).float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
+def test_cache_then_train_on_buckets(dev, tmp_path):
+    """images -> ARB buckets -> HIP VAE latent cache -> reader -> SD 1.5 train steps (mixed shapes)."""
+    from onetrainer_amd.dataLoader.aspect_bucketing import AspectBucketing
+    from onetrainer_amd.dataLoader.latent_cache import LatentCacheDataLoader, LatentCacheWriter
+    from onetrainer_amd.module import unet as U
+    from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util import create
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+    torch.manual_seed(0)
+    enc = V.AutoencoderKLEncoder(V.tiny_vae_config(), dev, seed=1)
+    ab = AspectBucketing(128, 64)
+    shapes = [(128, 128), (120, 130), (100, 170), (170, 100), (128, 200), (200, 128), (96, 96), (140, 140)]
+    samples = [{"image": torch.rand(3, h, w), "text": {"text_encoder_hidden_state": torch.randn(77, 96).bfloat16()}}
+               for h, w in shapes]
+    LatentCacheWriter(lambda im: enc.encode(im), str(tmp_path), ab, dev, encode_batch=4).write(samples)
+    cfg = TrainConfig.default_values()
+    cfg.model_type = "STABLE_DIFFUSION_15"
+    cfg.batch_size = 2
+    cfg.learning_rate_warmup_steps = 0
+    model = create.create_model(cfg, dev, seed=3, unet_config=U.tiny_sd15_config())
+    dl = LatentCacheDataLoader(str(tmp_path), batch_size=2, device=dev, seed=0)
+    tr = GenericTrainer(cfg, model=model, data_loader=dl)
+    tr.start()
+    dl.get_data_set().start_next_epoch()
+    shapes_seen = set()
+    for batch in dl.get_data_loader():
+        loss = tr.train_step(batch)
+        assert torch.isfinite(loss).item()
+        shapes_seen.add(tuple(batch["latent_image"].shape))
+    assert len(shapes_seen) >= 2
