@@ -66,6 +66,19 @@ typedef struct AttnArgs {
   int qsplit, pad_;
 } AttnArgs;
 
+/* FLUX q/k RMSNorm + rotary embedding over 128-wide heads (csrc/flux.hip) */
+typedef struct QKRopeArgs {
+  const void* x; long long ldx; int qoff, koff;
+  void* y; long long ldy; int yqoff, ykoff;
+  const void* dy; long long lddy; int dyqoff, dykoff;
+  const void *wq, *wk, *wq_ctx, *wk_ctx;
+  const float *cs, *sn;
+  float* dw_part;
+  int rows, B, H, L;
+  float eps;
+  int pad_;
+} QKRopeArgs;
+
 typedef struct AdamwGroup {
   long long begin, end;
   float wd_factor, one_minus_beta1, beta2, one_minus_beta2, bc2_sqrt, eps, neg_step_size, pad;
@@ -113,6 +126,49 @@ int otamd_softmax_rows_bwd(const void* P, long long ldp, const float* dP, long l
    (StableDiffusionXLBaseDataLoader.py:66-67): out[b,h,w,c] = img[b,c,h,w] * mul + add, NHWC bf16, c >= C zero */
 int otamd_image_to_nhwc(const float* img, int B, int C, int H, int W, float mul, float add, void* out, int cpad,
                         hipStream_t s);
+
+/* ---- FLUX.1 transformer (rows r = t * B + b over [text ; image] tokens; modulation mod[b * ldm + off + c]) ---- */
+/* replaces: AdaLayerNormZero / AdaLayerNormZeroSingle / AdaLayerNormContinuous forward (diffusers FluxTransformer2DModel,
+   called at modules/modelSetup/BaseFluxSetup.py:289-299): y = LN(x) * (1 + scale[b]) + shift[b], no affine */
+int otamd_adaln_fwd(const void* x, long long ldx, void* y, long long ldy, int rows, int D, float eps, const void* mod,
+                    long long ldm, int shift_off, int scale_off, int B, float* mean, float* rstd, hipStream_t s);
+
+/* replaces: autograd of that adaLN: dx, and bf16 d(shift), d(scale) written into dmod (part: otamd_mod_part_floats) */
+int otamd_adaln_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long lddx, int rows,
+                    int D, const void* mod, long long ldm, int shift_off, int scale_off, int B, const float* mean,
+                    const float* rstd, void* dmod, float* part, hipStream_t s);
+
+/* scratch floats the adaLN / gated-add backward reductions need */
+long long otamd_mod_part_floats(int T, int D, int B);
+
+/* replaces: hidden = hidden + gate_msa.unsqueeze(1) * attn_output (and the gate_mlp / single-block gate adds) */
+int otamd_gated_add_fwd(const void* x, long long ldx, const void* y, long long ldy, void* out, long long ldo, int rows,
+                        int D, const void* mod, long long ldm, int gate_off, int B, hipStream_t s);
+
+/* replaces: autograd of the gated add: dy = gate * dout, d(gate) into dmod */
+int otamd_gated_add_bwd(const void* dout, long long lddo, const void* y, long long ldy, void* dy, long long lddy,
+                        int rows, int D, const void* mod, long long ldm, int gate_off, int B, void* dmod, float* part,
+                        hipStream_t s);
+
+/* replaces: ABI check */
+int otamd_qk_rope_args_size(void);
+
+/* replaces: attn.norm_q / norm_k / norm_added_q / norm_added_k (RMSNorm eps 1e-6) + apply_rotary_emb(FluxPosEmbed) */
+int otamd_qknorm_rope_fwd(const QKRopeArgs* in, hipStream_t s);
+
+/* replaces: autograd of that; optional norm-weight grads (part: >= 512 * 1024 floats) */
+int otamd_qknorm_rope_bwd(const QKRopeArgs* in, void* dwq, void* dwk, void* dwq_ctx, void* dwk_ctx, int dw_f32,
+                          int dw_acc, float* part, hipStream_t s);
+
+/* replaces: GELU(approximate="tanh") of FeedForward(activation_fn="gelu-tanh") and the single blocks' act_mlp */
+int otamd_gelu_tanh_fwd(const void* x, long long ldx, void* y, long long ldy, int rows, int F, hipStream_t s);
+
+/* replaces: autograd of GELU(tanh) */
+int otamd_gelu_tanh_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long lddx,
+                        int rows, int F, hipStream_t s);
+
+/* replaces: FluxModel.pack_latents (dir 0) / unpack_latents (dir 1), modules/model/FluxModel.py:317-344 */
+int otamd_flux_pack(const void* src, void* dst, int B, int h, int w, int C, int ldl, int dir, hipStream_t s);
 
 /* replaces: ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out (diffusers, via BaseStableDiffusionXLSetup.py:268-273) */
 int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long long ldy, int N, int HW, int C, int G,

@@ -63,6 +63,16 @@ class AttnArgs(C.Structure):
                 ("scale", C.c_float), ("qsplit", C.c_int), ("pad_", C.c_int)]
 
 
+class QKRopeArgs(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("ldx", C.c_longlong), ("qoff", C.c_int), ("koff", C.c_int),
+                ("y", C.c_void_p), ("ldy", C.c_longlong), ("yqoff", C.c_int), ("ykoff", C.c_int),
+                ("dy", C.c_void_p), ("lddy", C.c_longlong), ("dyqoff", C.c_int), ("dykoff", C.c_int),
+                ("wq", C.c_void_p), ("wk", C.c_void_p), ("wq_ctx", C.c_void_p), ("wk_ctx", C.c_void_p),
+                ("cs", C.c_void_p), ("sn", C.c_void_p), ("dw_part", C.c_void_p),
+                ("rows", C.c_int), ("B", C.c_int), ("H", C.c_int), ("L", C.c_int), ("eps", C.c_float),
+                ("pad_", C.c_int)]
+
+
 VP, I, LL, F, D = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
 U64 = C.c_ulonglong
 
@@ -106,6 +116,18 @@ SIGNATURES: dict[str, list] = {
     "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
     "otamd_add": [VP, VP, VP, LL, VP],
     "otamd_image_to_nhwc": [VP, I, I, I, I, F, F, VP, I, VP],
+    # flux.hip
+    "otamd_adaln_fwd": [VP, LL, VP, LL, I, I, F, VP, LL, I, I, I, VP, VP, VP],
+    "otamd_adaln_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, LL, I, I, I, VP, VP, VP, VP, VP],
+    "otamd_mod_part_floats": [I, I, I],
+    "otamd_gated_add_fwd": [VP, LL, VP, LL, VP, LL, I, I, VP, LL, I, I, VP],
+    "otamd_gated_add_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, LL, I, I, VP, VP, VP],
+    "otamd_qk_rope_args_size": [],
+    "otamd_qknorm_rope_fwd": [C.POINTER(QKRopeArgs), VP],
+    "otamd_qknorm_rope_bwd": [C.POINTER(QKRopeArgs), VP, VP, VP, VP, I, I, VP, VP],
+    "otamd_gelu_tanh_fwd": [VP, LL, VP, LL, I, I, VP],
+    "otamd_gelu_tanh_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP],
+    "otamd_flux_pack": [VP, VP, I, I, I, I, I, I, VP],
     # diffusion.hip
     "otamd_noise": [VP, I, LL, LL, U64, VP],
     "otamd_timesteps": [VP, I, LL, U64, I, I, F, F, F, F, F, VP],
@@ -129,7 +151,7 @@ def lib():
         for name, args in SIGNATURES.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_plan")) else C.c_int
+            fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_plan", "_part_floats")) else C.c_int
         _lib = L
     return _lib
 
@@ -145,3 +167,4 @@ def check_layouts():
     assert L.otamd_conv_geom_size() == C.sizeof(ConvGeom)
     assert L.otamd_attn_args_size() == C.sizeof(AttnArgs), (L.otamd_attn_args_size(), C.sizeof(AttnArgs))
     assert L.otamd_lora_shadow_entry_size() == C.sizeof(LoraShadowEntry)
+    assert L.otamd_qk_rope_args_size() == C.sizeof(QKRopeArgs), (L.otamd_qk_rope_args_size(), C.sizeof(QKRopeArgs))

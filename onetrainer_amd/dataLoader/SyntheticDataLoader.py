@@ -60,3 +60,18 @@ class SyntheticDataLoader:
             else:
                 yield synthetic_sdxl_batch(self.batch_size, self.height, self.width, self.device, self.seed + i,
                                            sdxl=self.sdxl)
+
+
+def synthetic_flux_batch(batch_size, height, width, device, seed=0, latent_dtype=torch.float32, channels=16,
+                         scaling_factor=0.3611, shift_factor=0.1159, t5_dim=4096, pooled_dim=768, text_len=77):
+    """Flux output names (FluxBaseDataLoader): latent ~ N(0,1)/sf + shift so the scaled latent is N(0,1)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    h, w = height // 8, width // 8
+    lat = (torch.randn(batch_size, h, w, channels, generator=g) / scaling_factor + shift_factor).to(device, latent_dtype)
+    return {
+        "latent_image": lat,
+        "text_encoder_1_pooled_state": torch.randn(batch_size, pooled_dim, generator=g).to(device, torch.bfloat16),
+        "text_encoder_2_hidden_state": torch.randn(batch_size, text_len, t5_dim, generator=g).to(device, torch.bfloat16),
+        "loss_weight": torch.ones(batch_size, device=device),
+        "concept_type": ["STANDARD"] * batch_size,
+    }

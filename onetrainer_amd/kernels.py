@@ -788,3 +788,157 @@ def mse_grad(pred, target, coef, grad_out=None):
     check(lib().otamd_mse_grad(_p(pred), cpad, _p(target), int(target.dtype == F32), B, H * W, C_, _p(coef),
                                _p(grad_out), _p(dpred), stream_handle()), "otamd_mse_grad")
     return dpred
+
+
+# ------------------------------------------------------------------------------------------
+# FLUX.1 transformer ops (csrc/flux.hip).  Rows are r = t * B + b; `mod` is the [B, ldm] bf16
+# modulation output (shift / scale / gate chunks at column offsets).
+def _mod_ok(mod, B, *offs):
+    _req(mod.dtype == BF16 and mod.dim() == 2 and mod.shape[0] == B and mod.stride(1) == 1 and mod.stride(0) % 8 == 0,
+         "modulation: bf16 [B, ldm]")
+    for o in offs:
+        _req(o % 8 == 0 and o >= 0, "modulation chunk offsets must be multiples of 8")
+
+
+def _mod_part(T, D, B, device):
+    n = lib().otamd_mod_part_floats(T, D, B)
+    return workspace(n * 4, device)
+
+
+def adaln_fwd(x, mod, shift_off, scale_off, B, eps=1e-6, out=None):
+    rows, D, ldx = _rows2d(x)
+    _mod_ok(mod, B, shift_off, scale_off)
+    _req(shift_off + D <= mod.shape[1] and scale_off + D <= mod.shape[1], "modulation chunk range")
+    if out is None:
+        out = torch.empty((rows, D), dtype=BF16, device=x.device)
+    _, _, ldy = _rows2d(out)
+    mean = torch.empty(rows, dtype=F32, device=x.device)
+    rstd = torch.empty(rows, dtype=F32, device=x.device)
+    check(lib().otamd_adaln_fwd(_p(x), ldx, _p(out), ldy, rows, D, float(eps), _p(mod), mod.stride(0), shift_off,
+                                scale_off, B, _p(mean), _p(rstd), stream_handle()), "otamd_adaln_fwd")
+    return out, (mean, rstd)
+
+
+def adaln_bwd(x, dy, mod, shift_off, scale_off, B, stats, dmod=None, dx=None):
+    rows, D, ldx = _rows2d(x)
+    _, _, lddy = _rows2d(dy)
+    _mod_ok(mod, B, shift_off, scale_off)
+    if dx is None:
+        dx = torch.empty((rows, D), dtype=BF16, device=x.device)
+    _, _, lddx = _rows2d(dx)
+    part = None
+    if dmod is not None:
+        _req(dmod.shape == mod.shape and dmod.stride() == mod.stride(), "dmod like mod")
+        part = _mod_part(rows // B, D, B, x.device)
+    mean, rstd = stats
+    check(lib().otamd_adaln_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, rows, D, _p(mod), mod.stride(0), shift_off,
+                                scale_off, B, _p(mean), _p(rstd), _p(dmod), _p(part), stream_handle()),
+          "otamd_adaln_bwd")
+    return dx
+
+
+def gated_add_fwd(x, y, mod, gate_off, B, out=None):
+    rows, D, ldx = _rows2d(x)
+    _, _, ldy = _rows2d(y)
+    _mod_ok(mod, B, gate_off)
+    if out is None:
+        out = torch.empty((rows, D), dtype=BF16, device=x.device)
+    _, _, ldo = _rows2d(out)
+    check(lib().otamd_gated_add_fwd(_p(x), ldx, _p(y), ldy, _p(out), ldo, rows, D, _p(mod), mod.stride(0), gate_off,
+                                    B, stream_handle()), "otamd_gated_add_fwd")
+    return out
+
+
+def gated_add_bwd(dout, y, mod, gate_off, B, dmod, dy=None):
+    rows, D, lddo = _rows2d(dout)
+    _, _, ldy = _rows2d(y)
+    _mod_ok(mod, B, gate_off)
+    _req(dmod.shape == mod.shape and dmod.stride() == mod.stride(), "dmod like mod")
+    if dy is None:
+        dy = torch.empty((rows, D), dtype=BF16, device=dout.device)
+    _, _, lddy = _rows2d(dy)
+    part = _mod_part(rows // B, D, B, dout.device)
+    check(lib().otamd_gated_add_bwd(_p(dout), lddo, _p(y), ldy, _p(dy), lddy, rows, D, _p(mod), mod.stride(0),
+                                    gate_off, B, _p(dmod), _p(part), stream_handle()), "otamd_gated_add_bwd")
+    return dy
+
+
+def _qk_args(x, qoff, koff, H, B, L, w, cs, sn, eps):
+    a = _lib.QKRopeArgs()
+    rows, _, ldx = _rows2d(x)
+    wq, wk, wqc, wkc = w
+    for t in (wq, wk) + ((wqc, wkc) if wqc is not None else ()):
+        _req(t.dtype == BF16 and t.numel() == 128 and t.is_contiguous(), "q/k norm weights: bf16 [128]")
+    _req(cs.dtype == F32 and sn.dtype == F32 and cs.shape == sn.shape and cs.shape[1] == 128 and cs.is_contiguous()
+         and sn.is_contiguous() and cs.shape[0] * B >= rows, "rotary tables: fp32 [T, 128]")
+    a.x, a.ldx, a.qoff, a.koff = _p(x), ldx, qoff, koff
+    a.wq, a.wk, a.wq_ctx, a.wk_ctx = _p(wq), _p(wk), _p(wqc), _p(wkc)
+    a.cs, a.sn = _p(cs), _p(sn)
+    a.rows, a.B, a.H, a.L, a.eps = rows, B, H, L, eps
+    return a
+
+
+def qknorm_rope_fwd(x, qoff, koff, H, B, L, w, cs, sn, eps=1e-6, out=None):
+    """q / k columns of x (rows r = t*B + b) -> RMSNorm(128) * w -> rotary; out [rows, 2*H*128] = [q' | k']."""
+    rows = x.numel() // x.shape[-1]
+    if out is None:
+        out = torch.empty((rows, 2 * H * 128), dtype=BF16, device=x.device)
+    a = _qk_args(x, qoff, koff, H, B, L, w, cs, sn, eps)
+    _, _, ldy = _rows2d(out)
+    a.y, a.ldy, a.yqoff, a.ykoff = _p(out), ldy, 0, H * 128
+    check(lib().otamd_qknorm_rope_fwd(C.byref(a), stream_handle()), "otamd_qknorm_rope_fwd")
+    return out
+
+
+def qknorm_rope_bwd(x, qoff, koff, dy, H, B, L, w, cs, sn, dx, dxqoff, dxkoff, dw=(None, None, None, None),
+                    dw_acc=False, eps=1e-6):
+    """dy [rows, 2*H*128] (grads of [q' | k']) -> dx written at columns dxqoff / dxkoff of dx;
+    dw: grads of (wq, wk, wq_ctx, wk_ctx) or None each."""
+    a = _qk_args(x, qoff, koff, H, B, L, w, cs, sn, eps)
+    _, _, lddy = _rows2d(dy)
+    _, _, lddx = _rows2d(dx)
+    a.dy, a.lddy, a.dyqoff, a.dykoff = _p(dy), lddy, 0, H * 128
+    a.y, a.ldy, a.yqoff, a.ykoff = _p(dx), lddx, dxqoff, dxkoff
+    need = any(t is not None for t in dw)
+    f32 = int(any(t is not None and t.dtype == F32 for t in dw))
+    part = workspace(512 * 1024 * 4, x.device) if need else None
+    check(lib().otamd_qknorm_rope_bwd(C.byref(a), *[_p(t) for t in dw], f32, int(dw_acc), _p(part), stream_handle()),
+          "otamd_qknorm_rope_bwd")
+    return dx
+
+
+def gelu_tanh_fwd(x, out=None):
+    rows, F_, ldx = _rows2d(x)
+    if out is None:
+        out = torch.empty((rows, F_), dtype=BF16, device=x.device)
+    _, _, ldy = _rows2d(out)
+    check(lib().otamd_gelu_tanh_fwd(_p(x), ldx, _p(out), ldy, rows, F_, stream_handle()), "otamd_gelu_tanh_fwd")
+    return out
+
+
+def gelu_tanh_bwd(x, dy, dx=None):
+    rows, F_, ldx = _rows2d(x)
+    _, _, lddy = _rows2d(dy)
+    if dx is None:
+        dx = torch.empty((rows, F_), dtype=BF16, device=x.device)
+    _, _, lddx = _rows2d(dx)
+    check(lib().otamd_gelu_tanh_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, rows, F_, stream_handle()),
+          "otamd_gelu_tanh_bwd")
+    return dx
+
+
+def flux_pack(lat):
+    """NHWC latent [B, h, w, C] (bf16, row stride >= C) -> packed tokens [(h/2)(w/2) * B, 4C], rows t*B + b."""
+    B, h, w, C_ = lat.shape
+    _req(lat.dtype == BF16 and lat.stride(-1) == 1 and lat.stride(2) >= C_ and lat.stride(1) == lat.stride(2) * w
+         and lat.stride(0) == lat.stride(1) * h, "latent: NHWC bf16")
+    out = torch.empty(((h // 2) * (w // 2) * B, 4 * C_), dtype=BF16, device=lat.device)
+    check(lib().otamd_flux_pack(_p(lat), _p(out), B, h, w, C_, lat.stride(2), 0, stream_handle()), "otamd_flux_pack")
+    return out
+
+
+def flux_unpack(tok, B, h, w, C_):
+    _req(tok.dtype == BF16 and tok.is_contiguous() and tok.shape == ((h // 2) * (w // 2) * B, 4 * C_), "packed tokens")
+    out = torch.empty((B, h, w, C_), dtype=BF16, device=tok.device)
+    check(lib().otamd_flux_pack(_p(tok), _p(out), B, h, w, C_, C_, 1, stream_handle()), "otamd_flux_pack")
+    return out

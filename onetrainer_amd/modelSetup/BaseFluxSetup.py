@@ -1,0 +1,103 @@
+"""predict / calculate_loss for FLUX.1 on the HIP kernels.
+
+Drop-in for modules/modelSetup/BaseFluxSetup.py:193-390 with the math of ModelSetupNoiseMixin
+(noise; LOGIT_NORMAL / UNIFORM timesteps, static or dynamic shift), ModelSetupFlowMatchingMixin.py:14-39
+(sigma = (t + 1) / N, x_t = sigma noise + (1 - sigma) x0), FluxModel.pack/unpack_latents and
+ModelSetupDiffusionLossMixin._flow_matching_losses (unmasked MSE, flow target noise - x0):
+  * latents arrive NHWC [B, h, w, 16] (this build's cache) or NCHW [B, 16, h, w];
+  * one prologue kernel does the shift / scale, the noising and the flow target;
+  * the transformer gets t / 1000 and guidance = prior.guidance_scale, like the reference.
+Batch contract: text_encoder_1_pooled_state [B, 768] (CLIP pooled), text_encoder_2_hidden_state
+[B, L, 4096] (T5), latent_image, loss_weight (FluxBaseDataLoader output names).
+"""
+from __future__ import annotations
+
+import math
+from random import Random
+
+import torch
+
+from .. import kernels as K
+from ..module import flux_ops as O
+from ..module import functional as Fn
+
+
+class BaseFluxSetup:
+    def __init__(self, train_device, temp_device=None, debug_mode=False, dp_rank=0, dp_world=1):
+        self.train_device = torch.device(train_device)
+        self.temp_device = temp_device
+        self.debug_mode = debug_mode
+        self.dp_rank = dp_rank
+        self.dp_world = dp_world
+
+    @staticmethod
+    def _nhwc_latent(lat: torch.Tensor) -> torch.Tensor:
+        if lat.dim() == 4 and lat.shape[1] == 16 and lat.shape[-1] != 16:
+            lat = lat.permute(0, 2, 3, 1)
+        return lat.contiguous()
+
+    def _text(self, batch, config, rand, B):
+        """FluxModel.encode_text with cached outputs: per-encoder dropout masks from Random(seed)."""
+        pooled = batch["text_encoder_1_pooled_state"]
+        ehs = batch["text_encoder_2_hidden_state"]
+        p1, p2 = config.text_encoder.dropout_probability, config.text_encoder_2.dropout_probability
+        if p1 is not None and p1 > 0:
+            m = torch.tensor([rand.random() > p1 for _ in range(B)], device=pooled.device).to(pooled.dtype)
+            pooled = pooled * m[:, None]
+        if p2 is not None and p2 > 0:
+            m = torch.tensor([rand.random() > p2 for _ in range(B)], device=ehs.device).to(ehs.dtype)
+            ehs = ehs * m[:, None, None]
+        return pooled.to(torch.bfloat16).contiguous(), ehs.to(torch.bfloat16).contiguous()
+
+    def _shift(self, config, h, w):
+        """ModelSetupNoiseMixin._get_timestep_discrete: static timestep_shift, or the dynamic one of the
+        image sequence length (base 256 -> 0.5, max 4096 -> 1.15, patch 2)."""
+        if not config.dynamic_timestep_shifting:
+            return config.timestep_shift
+        m = (1.15 - 0.5) / (4096 - 256)
+        mu = (w // 2) * (h // 2) * m + (0.5 - m * 256)
+        return math.exp(mu)
+
+    def predict(self, model, batch: dict, config, train_progress, *, deterministic: bool = False) -> dict:
+        if config.offset_noise_weight > 0 or config.perturbation_noise_weight > 0:
+            raise NotImplementedError("offset / perturbation noise are not on this build's hot path yet")
+        batch_seed = 0 if deterministic else train_progress.global_step
+        rand = Random(batch_seed)
+        latent = self._nhwc_latent(batch["latent_image"])
+        B, h, w, C = latent.shape
+        pooled, ehs = self._text(batch, config, rand, B)
+        sample0 = self.dp_rank * B
+        noise = K.noise(latent.shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=latent.dtype,
+                        device=latent.device)
+        N = model.noise_scheduler.config["num_train_timesteps"]
+        if deterministic:
+            timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=latent.device)
+        else:
+            dist = {"UNIFORM": 0, "LOGIT_NORMAL": 1}[config.timestep_distribution]
+            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=dist, num_train_timesteps=N,
+                                   min_s=config.min_noising_strength, max_s=config.max_noising_strength,
+                                   shift=self._shift(config, h, w), bias=config.noising_bias,
+                                   weight=config.noising_weight, device=latent.device)
+        vc = model.vae.config
+        model_in, target = K.flow_prologue(latent, noise, timestep, vc["scaling_factor"], vc["shift_factor"], N,
+                                           cpad=C)
+        tokens = K.flux_pack(model_in)
+        guidance = None
+        if model.transformer.config["guidance_embeds"]:
+            guidance = torch.full((B,), float(config.prior.guidance_scale), dtype=torch.float32, device=latent.device)
+        pred_tok = model.transformer(tokens, timestep.float() / 1000, guidance, pooled, ehs, h, w)
+        pred = O.UnpackFn.apply(pred_tok, B, h, w, C)
+        return {"loss_type": "target", "timestep": timestep, "predicted": pred, "target": target}
+
+    def calculate_loss(self, model, batch: dict, data: dict, config) -> torch.Tensor:
+        """_flow_matching_losses(...).mean() (BaseFluxSetup.py:377-390): unmasked MSE x loss_weight x scalers."""
+        if config.mae_strength != 0 or config.log_cosh_strength != 0 or config.masked_training:
+            raise NotImplementedError("only the unmasked MSE loss of C1-C5 is on this build's hot path")
+        if config.loss_weight_fn != "CONSTANT":
+            raise NotImplementedError(f"flow-matching loss weight {config.loss_weight_fn}")
+        bs = 1 if config.loss_scaler in ("NONE", "GRADIENT_ACCUMULATION") else config.batch_size
+        gas = 1 if config.loss_scaler in ("NONE", "BATCH") else config.gradient_accumulation_steps
+        lw = batch.get("loss_weight")
+        lw = lw.to(self.train_device, torch.float32).contiguous() if lw is not None else None
+        return Fn.MSELossFn.apply(data["predicted"], data["target"], lw, data["timestep"], None, 0, 5.0, False, 1.0,
+                                  config.mse_strength, float(bs * gas), 1.0 / self.dp_world)

@@ -133,11 +133,9 @@ class LoraLinearFn(torch.autograd.Function):
             dx = K.linear_dgrad(dy2, wref.w, lora=(u, site.down)).view(ctx.xshape)
         acc = site.acc()
         K.linear_wgrad(u, x2, out=site.g_down, accumulate=acc)
-        r, n0 = site.rank, 0
-        for p, g in enumerate(site.g_up):
-            n1 = n0 + g.shape[0]
+        r = site.rank
+        for p, (g, (n0, n1)) in enumerate(zip(site.g_up, site.ranges)):
             K.linear_wgrad(dy2[:, n0:n1], t[:, p * r:(p + 1) * r], out=g, accumulate=acc, alpha=site.scale)
-            n0 = n1
         site.done()
         if wref.trainable:
             K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())

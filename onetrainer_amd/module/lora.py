@@ -36,18 +36,21 @@ PRESETS = {"attn-mlp": ["attentions"], "attn-only": ["attn"], "full": []}   # St
 
 @dataclass
 class LoraSite:
-    """adapters of one base GEMM: P parts (P > 1 for a fused q|k|v or k|v projection)."""
+    """adapters of one base GEMM (a fused group: q|k|v, k|v, q|k|v|mlp ... or a single module).
+    Only the modules matching the layer filter carry adapters; the others are zero rows of `up2`."""
     key: str
-    modules: list            # reference module names, one per part
+    modules: list            # adapted module names (reference names), in fused order
     kind: str                # "linear" | "conv"
     cin: int                 # base input channels (store layout; conv_in padded)
-    couts: list              # per-part base output channels (store layout; conv_out padded)
+    couts: list              # per adapted module, base output channels (store layout)
     k: int                   # conv kernel size (1 for linear)
     cin_ref: int = 0         # diffusers input channels (unpadded)
     conv1x1: bool = False    # a 1x1 Conv2d held as a linear (diffusers NCHW [out, in, 1, 1] on export)
     couts_ref: list = field(default_factory=list)
+    ranges: list = field(default_factory=list)   # per adapted module, (n0, n1) output columns in the fused GEMM
+    n_total: int = 0         # fused GEMM output width
     down: torch.Tensor | None = None     # bf16 shadow [P*r, cin] or [r, k, k, cin]
-    up2: torch.Tensor | None = None      # bf16 shadow [sum(couts), P*r] (block-diagonal for P > 1), x alpha/r
+    up2: torch.Tensor | None = None      # bf16 shadow [n_total, P*r] (block-diagonal, zero rows elsewhere), x alpha/r
     g_down: torch.Tensor | None = None   # fp32 grad view, shape of `down`
     g_up: list = field(default_factory=list)   # fp32 grad views [cout_p, r]
     store: FlatParamStore | None = None
@@ -55,6 +58,7 @@ class LoraSite:
     scale: float = 1.0
     rank: int = 0
     params: tuple = ()
+    group: tuple = ()        # all modules of the base GEMM (adapted or not)
 
     def acc(self) -> bool:
         return self.store.accumulate_into(self.names)
@@ -63,15 +67,15 @@ class LoraSite:
         self.store.mark_ready(self.names)
 
 
-def _module_list(unet):
-    """(module name, kind, cin, cout, k, cin_ref, cout_ref) for every Linear/Conv2d of the UNet, in
-    forward order, from the base parameter specs (diffusers shapes) and the store layout."""
+def module_list(model):
+    """(module name, kind, cin, cout, k, cin_ref, cout_ref) for every Linear/Conv2d of a model with
+    `specs` (name, diffusers shape, kind, fan_in) and a FlatParamStore `store`, in forward order."""
     out = []
-    for name, shape, kind, _ in unet.specs:
+    for name, shape, kind, _ in model.specs:
         if not name.endswith(".weight") or kind not in ("linear", "conv"):
             continue
         mod = name[:-len(".weight")]
-        st = unet.store.slots[name].shape
+        st = model.store.slots[name].shape
         if kind == "linear":
             out.append((mod, "linear", st[1], st[0], 1, shape[1], shape[0]))
         elif len(st) == 2:           # 1x1 conv, held as a linear
@@ -81,44 +85,57 @@ def _module_list(unet):
     return out
 
 
-class LoRAUNetWrapper:
-    """LoRAModuleWrapper(unet, "lora_unet", config, module_filter) for the HIP UNet."""
+def unet_fused_group(name, by_name):
+    """the base GEMM a UNet module runs in (module/unet.py): attn1 q|k|v and attn2 k|v are fused."""
+    for suf in (".attn1.to_q", ".attn1.to_k", ".attn1.to_v"):
+        if name.endswith(suf):
+            b = name[:-len(suf)] + ".attn1."
+            return [b + "to_q", b + "to_k", b + "to_v"]
+    for suf in (".attn2.to_k", ".attn2.to_v"):
+        if name.endswith(suf):
+            b = name[:-len(suf)] + ".attn2."
+            return [b + "to_k", b + "to_v"]
+    return [name]
 
-    def __init__(self, unet, rank: int = 16, alpha: float = 1.0, module_filter=None, prefix: str = "lora_unet",
+
+class LoRAWrapper:
+    """LoRAModuleWrapper(model, prefix, config, module_filter) for a HIP model (UNet or Flux
+    transformer): the model supplies `specs`, `store`, `device` and optionally `fused_group(name, by_name)`."""
+
+    def __init__(self, model, rank: int = 16, alpha: float = 1.0, module_filter=None, prefix: str = "lora_unet",
                  seed: int = 0, dtype=torch.float32):
-        self.unet = unet
+        self.model = self.unet = model
         self.rank, self.alpha, self.prefix = rank, float(alpha), prefix
         self.scale = self.alpha / rank
         filt = [x.strip() for x in (module_filter or []) if x.strip()]
-        mods = [m for m in _module_list(unet) if not filt or any(f in m[0] for f in filt)]
-        by_name = {m[0]: m for m in mods}
-        # group fused projections exactly as the base UNet runs them
-        sites, used = [], set()
-        for m in mods:
-            name = m[0]
-            if name in used:
+        allmods = module_list(model)
+        by_name = {m[0]: m for m in allmods}
+        adapted = {m[0] for m in allmods if not filt or any(f in m[0] for f in filt)}
+        group_of = getattr(model, "fused_group", unet_fused_group)
+        sites, seen = [], set()
+        for m in allmods:
+            if m[0] in seen:
                 continue
-            group = [name]
-            if name.endswith(".attn1.to_q"):
-                b = name[:-len("to_q")]
-                if b + "to_k" in by_name and b + "to_v" in by_name:
-                    group = [b + "to_q", b + "to_k", b + "to_v"]
-            elif name.endswith(".attn2.to_k"):
-                b = name[:-len("to_k")]
-                if b + "to_v" in by_name:
-                    group = [b + "to_k", b + "to_v"]
-            parts = [by_name[g] for g in group]
-            used.update(group)
+            group = [g for g in group_of(m[0], by_name) if g in by_name]
+            seen.update(group)
+            mods = [g for g in group if g in adapted]
+            if not mods:
+                continue
+            n0, ranges = 0, {}
+            for g in group:
+                ranges[g] = (n0, n0 + by_name[g][3])
+                n0 += by_name[g][3]
             kind = "conv" if m[1] == "conv" else "linear"
             key = group[0] if len(group) == 1 else (group[0].rsplit(".", 1)[0] + "." + "|".join(
                 g.rsplit(".", 1)[1] for g in group))
-            sites.append(LoraSite(key=key, modules=group, kind=kind, cin=m[2], couts=[p[3] for p in parts], k=m[4],
-                                  cin_ref=m[5], couts_ref=[p[6] for p in parts], scale=self.scale, rank=rank,
-                                  conv1x1=m[1] == "linear1x1"))
+            sites.append(LoraSite(key=key, modules=mods, kind=kind, cin=m[2], couts=[by_name[g][3] for g in mods],
+                                  k=m[4], cin_ref=m[5], couts_ref=[by_name[g][6] for g in mods], scale=self.scale,
+                                  rank=rank, conv1x1=m[1] == "linear1x1", ranges=[ranges[g] for g in mods],
+                                  n_total=n0, group=tuple(group)))
         self.sites = sites
         self.site_of = {}
         for s in sites:
-            for mname in s.modules:
+            for mname in s.group:
                 self.site_of[mname] = s
             self.site_of[s.key] = s
         # fp32 store: per site, downs adjacent (fused operand), then ups
@@ -126,28 +143,28 @@ class LoRAUNetWrapper:
         for s in sites:
             for mname in s.modules:
                 dshape = (rank, s.cin) if s.kind == "linear" else (rank, s.k, s.k, s.cin)
-                specs.append((f"{prefix}.{mname}.lora_down.weight", dshape, "unet_lora"))
+                specs.append((f"{prefix}.{mname}.lora_down.weight", dshape, prefix))
             for mname, co in zip(s.modules, s.couts):
-                specs.append((f"{prefix}.{mname}.lora_up.weight", (co, rank), "unet_lora"))
-        self.store = FlatParamStore(specs, dtype, torch.device(unet.device))
+                specs.append((f"{prefix}.{mname}.lora_up.weight", (co, rank), prefix))
+        self.store = FlatParamStore(specs, dtype, torch.device(model.device))
         # bf16 shadow: per site the fused down then the block-diagonal up
         total = 0
         layout = []
         for s in sites:
             P = len(s.modules)
             dn = P * rank * s.cin * s.k * s.k
-            un = sum(s.couts) * P * rank
+            un = s.n_total * P * rank
             doff = (total + 7) // 8 * 8
             uoff = (doff + dn + 7) // 8 * 8
             total = uoff + un
             layout.append((doff, uoff))
-        self.shadow = torch.zeros(total + 8, dtype=torch.bfloat16, device=unet.device)
+        self.shadow = torch.zeros(total + 8, dtype=torch.bfloat16, device=model.device)
         entries = []
         for s, (doff, uoff) in zip(sites, layout):
             P = len(s.modules)
             dshape = (P * rank, s.cin) if s.kind == "linear" else (rank, s.k, s.k, s.cin)
             s.down = self.shadow[doff:doff + math.prod(dshape)].view(dshape)
-            s.up2 = self.shadow[uoff:uoff + sum(s.couts) * P * rank].view(sum(s.couts), P * rank)
+            s.up2 = self.shadow[uoff:uoff + s.n_total * P * rank].view(s.n_total, P * rank)
             s.store = self.store
             s.names = [f"{prefix}.{m}.lora_down.weight" for m in s.modules] + \
                       [f"{prefix}.{m}.lora_up.weight" for m in s.modules]
@@ -156,19 +173,25 @@ class LoRAUNetWrapper:
             s.params = tuple(self.store.params[n] for n in s.names)
             dslot = self.store.slots[s.names[0]]
             entries.append((dslot.offset, doff, P * rank, dslot.numel // rank, dslot.numel // rank, 1.0))
-            row0 = 0
             for p in range(P):
                 us = self.store.slots[s.names[P + p]]
-                entries.append((us.offset, uoff + row0 * P * rank + p * rank, s.couts[p], rank, P * rank, self.scale))
-                row0 += s.couts[p]
+                entries.append((us.offset, uoff + s.ranges[p][0] * P * rank + p * rank, s.couts[p], rank, P * rank,
+                                self.scale))
         arr = (_lib.LoraShadowEntry * len(entries))()
         for i, (src, dst, rows, cols, ld, sc) in enumerate(entries):
             arr[i].src, arr[i].dst, arr[i].rows, arr[i].cols, arr[i].dst_ld, arr[i].scale = src, dst, rows, cols, ld, sc
-        self._table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(unet.device)
+        self._table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(model.device)
         self._n_entries = len(entries)
         if seed is not None:
             self.init_weights(seed)
         self.refresh()
+
+    def site_for(self, modules):
+        """site of the base GEMM running `modules` (None when none of them carries an adapter)."""
+        s = self.site_of.get(modules[0])
+        if s is not None and tuple(modules) != s.group:
+            raise NotImplementedError(f"base GEMM {modules} does not match the LoRA fusion group {s.group}")
+        return s
 
     # ----- parameters ----------------------------------------------------------------------------
     def init_weights(self, seed: int):
@@ -242,3 +265,6 @@ class LoRAUNetWrapper:
                     pu.zero_()
                     pu[:co_ref].copy_(u.reshape(co_ref, self.rank))
         self.refresh()
+
+
+LoRAUNetWrapper = LoRAWrapper   # the UNet form (prefix "lora_unet")

@@ -284,13 +284,8 @@ class UNet2DConditionModel:
         return self.lora.site_of.get(module) if self.lora is not None else None
 
     def _lo_fused(self, modules):
-        """site of a fused base GEMM (to_q|to_k|to_v, to_k|to_v): all parts adapted or none."""
-        sites = [self._lo(m) for m in modules]
-        if all(s is None for s in sites):
-            return None
-        if any(s is None or s.modules != list(modules) for s in sites):
-            raise NotImplementedError(f"LoRA layer filter adapts only part of the fused projection {modules}")
-        return sites[0]
+        """site of a fused base GEMM (to_q|to_k|to_v, to_k|to_v)."""
+        return self.lora.site_for(list(modules)) if self.lora is not None else None
 
     def _linear(self, x, p, bias=True, residual=None):
         return Fn.linear(x, self.R(p + ".weight"), self.R(p + ".bias") if bias else None, residual, lora=self._lo(p))

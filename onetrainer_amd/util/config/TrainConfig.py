@@ -31,6 +31,8 @@ class ModelPartConfig:
     learning_rate: float | None = None
     weight_dtype: str = "NONE"
     dropout_probability: float = 0.0
+    guidance_scale: float = 1.0          # prior (Flux) only: TrainConfig.py:228
+    attention_mask: bool = False
 
 
 @dataclass

@@ -12,10 +12,20 @@ from ..util.lr_scheduler_util import create_lr_scheduler  # noqa: F401  (re-expo
 SCALING = {"STABLE_DIFFUSION_XL_10_BASE": 0.13025, "STABLE_DIFFUSION_15": 0.18215}
 
 
-def create_model(config, device, seed=0, unet_config=None, prediction_type="epsilon"):
+def is_flux(model_type: str) -> bool:
+    return model_type.startswith("FLUX")
+
+
+def create_model(config, device, seed=0, unet_config=None, prediction_type="epsilon", flux_config=None):
     """random-weight model of the configured architecture (weights from disk: SURVEY.md §8(f) #2).
-    LoRA training keeps the base UNet frozen (no gradient buffer)."""
+    LoRA training keeps the base network frozen (no gradient buffer)."""
     mt = config.model_type
+    if is_flux(mt):
+        from ..model.FluxModel import FluxModel
+        from ..module import flux as FX
+        tr = FX.FluxTransformer2DModel(flux_config or FX.flux_dev_config(), device, seed=seed,
+                                       trainable=config.training_method != "LORA")
+        return FluxModel(tr, model_type=mt)
     if unet_config is None:
         if mt.startswith("STABLE_DIFFUSION_XL"):
             unet_config = U.sdxl_config()
@@ -34,6 +44,14 @@ def is_sd15(model_type: str) -> bool:
 
 def create_model_setup(config, train_device, dp_rank=0, dp_world=1):
     """ModelType x TrainingMethod -> plugin (create.py:285-353)."""
+    if is_flux(config.model_type):
+        if config.training_method == "LORA":
+            from ..modelSetup.FluxLoRASetup import FluxLoRASetup as S
+        elif config.training_method == "FINE_TUNE":
+            from ..modelSetup.FluxFineTuneSetup import FluxFineTuneSetup as S
+        else:
+            raise NotImplementedError(f"training method {config.training_method}")
+        return S(train_device, dp_rank=dp_rank, dp_world=dp_world)
     sd15 = is_sd15(config.model_type)
     if not sd15 and not config.model_type.startswith("STABLE_DIFFUSION_XL"):
         raise NotImplementedError(f"model type {config.model_type}")

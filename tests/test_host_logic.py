@@ -106,3 +106,43 @@ def test_vae_encoder_spec_and_flops():
     om = OV.AutoencoderKLEncoder(cfg)
     assert {n for n, *_ in specs} == set(om.state_dict())
     assert sum(math.prod(s) for _, s, _, _ in specs) == sum(p.numel() for p in om.parameters()) == 34_163_664
+
+
+def test_flux_spec_and_flops():
+    """SURVEY.md Appendix B: FLUX@768 34.71 TF, @1024 66.07 TF forward; FLUX.1-dev 11.9 B params;
+    parameter names equal the oracle's (diffusers FluxTransformer2DModel); RoPE tables match."""
+    import numpy as np
+    import torch
+    from onetrainer_amd.module import flux as FX
+    from oracle import flux as OF
+    c = FX.flux_dev_config()
+    assert abs(FX.flops_per_image(c, 2304) / 1e12 - 34.71) < 5e-3
+    assert abs(FX.flops_per_image(c, 4096) / 1e12 - 66.07) < 1e-2
+    assert sum(math.prod(s) for _, s, _, _ in FX.flux_specs(c)) == 11_901_408_320
+    t = FX.tiny_flux_config()
+    om = OF.FluxTransformer2DModel(OF.tiny_flux_config())
+    assert {n for n, *_ in FX.flux_specs(t)} == set(om.state_dict())
+    cs, sn = FX.rope_tables(5, 8, 6, t)
+    c2, s2 = OF.rope_tables(torch.cat([torch.zeros(5, 3), OF.prepare_latent_image_ids(8, 6)]), t.axes_dims_rope)
+    assert np.abs(cs - c2.numpy()).max() < 1e-6 and np.abs(sn - s2.numpy()).max() < 1e-6
+
+
+def test_flux_lora_groups():
+    """LoRA fusion groups of the Flux transformer (module/lora.py): q|k|v, add_q|k|v, single-block
+    q|k|v|proj_mlp, norm1|norm1_context; 'attn-mlp' adapts q|k|v but not proj_mlp (zero rows)."""
+    import torch
+    from onetrainer_amd.module import flux as FX
+    from onetrainer_amd.module.lora import LoRAWrapper
+    m = FX.FluxTransformer2DModel(FX.tiny_flux_config(), "cpu", seed=None)
+    w = LoRAWrapper(m, rank=4, module_filter=["attn", "ff.net"], prefix="lora_transformer", seed=None)
+    s = w.site_of["single_transformer_blocks.0.proj_mlp"]
+    assert s.modules == ["single_transformer_blocks.0.attn.to_q", "single_transformer_blocks.0.attn.to_k",
+                         "single_transformer_blocks.0.attn.to_v"]
+    assert s.n_total == 7 * 256 and s.ranges[2] == (512, 768)
+    assert "transformer_blocks.0.ff_context.net.0.proj" not in w.site_of
+    assert w.site_for(["transformer_blocks.1.attn.add_q_proj", "transformer_blocks.1.attn.add_k_proj",
+                       "transformer_blocks.1.attn.add_v_proj"]) is not None
+    full = LoRAWrapper(m, rank=4, prefix="lora_transformer", seed=None)
+    assert full.site_of["transformer_blocks.0.norm1.linear"].group == (
+        "transformer_blocks.0.norm1.linear", "transformer_blocks.0.norm1_context.linear")
+    del torch
