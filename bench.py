@@ -113,8 +113,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 4 sdxl / 16 sd15)")
     ap.add_argument("--res", type=int, default=None, help="default 1024 (sdxl) / 512 (sd15)")
-    ap.add_argument("--model", choices=["sdxl", "sd15"], default="sdxl",
-                    help="sdxl: configs[2] per GPU (metric workload); sd15: configs[1] (SD 1.5 512^2 b=16)")
+    ap.add_argument("--model", choices=["sdxl", "sd15", "flux"], default="sdxl",
+                    help="sdxl: configs[2] per GPU (metric workload); sd15: configs[1] (SD 1.5 512^2 b=16); "
+                         "flux: configs[4] per GPU (FLUX.1 LoRA r16, 768^2, b=4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true", help="skip the VAE-encode (latent caching) side measurement")
     ap.add_argument("--cpu-res", type=int, default=512)
@@ -126,14 +127,19 @@ def main():
     from onetrainer_amd.util.config.TrainConfig import TrainConfig
 
     sd15 = args.model == "sd15"
+    flux = args.model == "flux"
     if args.res is None:
-        args.res = 512 if sd15 else 1024
+        args.res = 512 if sd15 else (768 if flux else 1024)
     if args.batch is None:
         args.batch = 16 if sd15 else 4
     ucfg = sd15_config() if sd15 else sdxl_config()
     cfg = TrainConfig.default_values()
     if sd15:
         cfg.model_type = "STABLE_DIFFUSION_15"
+    if flux:   # training_presets/#flux LoRA.json: LORA, LOGIT_NORMAL, lr 3e-4 (base bf16: NF4 is CUDA-only)
+        cfg.model_type, cfg.training_method = "FLUX_DEV_1", "LORA"
+        cfg.timestep_distribution = "LOGIT_NORMAL"
+        args.no_vae = True
     cfg.batch_size = args.batch
     cfg.learning_rate = 3e-6
     cfg.learning_rate_warmup_steps = 0
@@ -144,10 +150,15 @@ def main():
     tr.start()
     rank, world = tr.rank, tr.world
     dev = tr.device
+    net = tr.model.transformer if flux else tr.model.unet
     log(f"[bench] rank {rank}/{world} model ready in {time.time() - t0:.1f}s "
-        f"({tr.model.unet.num_parameters() / 1e9:.3f} B params)")
-    batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=rank, sdxl=not sd15,
-                                 scaling_factor=0.18215 if sd15 else 0.13025)
+        f"({net.num_parameters() / 1e9:.3f} B params)")
+    if flux:
+        from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_flux_batch
+        batch = synthetic_flux_batch(args.batch, args.res, args.res, dev, seed=rank)
+    else:
+        batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=rank, sdxl=not sd15,
+                                     scaling_factor=0.18215 if sd15 else 0.13025)
 
     for i in range(args.warmup):
         tr.train_step(batch)
@@ -195,12 +206,29 @@ def main():
     imgs = args.batch * world * args.steps
     value = imgs / elapsed
     ms = 1000.0 * elapsed / args.steps
-    fwd_tf = flops_per_image(ucfg, args.res // 8, args.res // 8) / 1e12
-    train_tf_img = 3.0 * fwd_tf                       # fwd + dgrad + wgrad
+    if flux:   # LoRA: 2 x base forward (fwd + dgrad, frozen base) + 3 x LoRA branch
+        from onetrainer_amd.module import flux as FX
+        n_img = (args.res // 16) ** 2
+        fwd_tf = FX.flops_per_image(net.cfg, n_img, 77) / 1e12
+        lora_tf = 2.0 * FX.lora_macs_per_image(tr.model.transformer_lora, 77, n_img) / 1e12
+        train_tf_img = 2.0 * fwd_tf + 3.0 * lora_tf
+        basis = f"{train_tf_img:.3f} TFLOP/image algorithmic (2 x {fwd_tf:.3f} base fwd + 3 x {lora_tf:.3f} LoRA)"
+    else:
+        fwd_tf = flops_per_image(ucfg, args.res // 8, args.res // 8) / 1e12
+        train_tf_img = 3.0 * fwd_tf                       # fwd + dgrad + wgrad
+        basis = f"{train_tf_img:.3f} TFLOP/image algorithmic (3 x {fwd_tf:.3f} fwd)"
     achieved = train_tf_img * args.batch / (ms / 1000.0)   # per GPU, TFLOP/s
     mname = "SD 1.5 UNet (859.5M params)" if sd15 else "SDXL 1.0 UNet (2.567B params)"
+    label = "SD1.5 512^2 bf16" if sd15 else "SDXL 1024^2 bf16"
+    wl = f"{'SD 1.5' if sd15 else 'SDXL 1.0'} UNet full fine-tune train step {args.res}^2 (latent {args.res // 8}^2), " \
+         f"b={args.batch}/GPU, AdamW+bf16 SR, clip 1.0"
+    if flux:
+        mname = "FLUX.1-dev transformer (11.9B params, bf16 base) + LoRA r16 (all Linear)"
+        label = f"FLUX.1 LoRA {args.res}^2 bf16"
+        wl = f"FLUX.1 LoRA rank {cfg.lora_rank} train step {args.res}^2 (latent {args.res // 8}^2 -> {(args.res // 16) ** 2} " \
+             f"tokens + 77 text), b={args.batch}/GPU, flow matching LOGIT_NORMAL, fp32 AdamW, clip 1.0"
     out = {
-        "metric": "train images/sec (whole node) + step-time p50, " + ("SD1.5 512^2 bf16" if sd15 else "SDXL 1024^2 bf16"),
+        "metric": "train images/sec (whole node) + step-time p50, " + label,
         "value": round(value, 3),
         "unit": "images/s",
         "n_gpus": world,
@@ -214,8 +242,7 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random cached latents/text states, random-init weights)",
-        "config": {"workload": f"{'SD 1.5' if sd15 else 'SDXL 1.0'} UNet full fine-tune train step {args.res}^2 "
-                               f"(latent {args.res // 8}^2), b={args.batch}/GPU, AdamW+bf16 SR, clip 1.0",
+        "config": {"workload": wl,
                    "model": mname, "global_batch": args.batch * world,
                    "seq_len": (args.res // 8) ** 2, "parallelism": f"dp{world}"},
         "loss": round(loss_val, 5),
@@ -225,12 +252,11 @@ def main():
                      "basis": f"sum(2*M*N*K) over the {g_n} GEMM/conv launches of one step / sum of their HIP-event "
                               f"durations ({g_ms:.2f} ms of GEMM per step)",
                      "step_achieved": round(achieved, 1), "step_frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                     "step_basis": f"{train_tf_img:.3f} TFLOP/image algorithmic (3 x {fwd_tf:.3f} fwd) x per-GPU "
-                                   "images / step time"},
+                     "step_basis": basis + " x per-GPU images / step time"},
         "cpu_baseline": None,
         "vae_encode": vae,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not flux:
         del tr
         torch.cuda.empty_cache()
         log("[bench] cpu baseline (oracle, fp32) ...")

@@ -431,8 +431,10 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 
 // dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of 32 in this split's range.
 // Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 {lse, delta} pairs.
+// D = 128: the dK/dV accumulators alone take 128 VGPRs and the 3-deep ring (99 KiB) already limits a
+// CU to one block, so the full 512-entry register file is used instead of spilling at 256.
 template <int D>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = QT * D * 2;                 // one [32 x D] image
   constexpr int STG = 4 * TB + QT * 8;           // + 32 float2 pairs

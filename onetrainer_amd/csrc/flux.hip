@@ -429,10 +429,12 @@ OTAMD_API int otamd_adaln_fwd(const void* x, long long ldx, void* y, long long l
   return OTAMD_OK;
 }
 
+// token splits of the per-sample column reductions: >= 64 tokens per thread (the slab the reduce
+// pass re-reads stays small), and enough blocks to cover the CUs
 static int mod_splits(int T, int D, int B) {
   const int xb = (D / 8 + 255) / 256;
-  int S = std::max(1, 2048 / std::max(1, xb * B));
-  S = std::min(S, std::max(1, (T + 7) / 8));
+  int S = std::max(1, 512 / std::max(1, xb * B));
+  S = std::min(S, std::max(1, (T + 63) / 64));
   return S;
 }
 

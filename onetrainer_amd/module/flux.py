@@ -342,3 +342,25 @@ class FluxTransformer2DModel:
         return self._linear(n, "proj_out")
 
     __call__ = forward
+
+
+def rows_per_image(module: str, L: int, N: int) -> int:
+    """token rows one image contributes to a module's GEMM (text stream L, image stream N, both L + N,
+    modulation / time embedders 1)."""
+    if module.startswith("time_text_embed.") or module.endswith(".norm1.linear") or \
+            module.endswith(".norm1_context.linear") or module.endswith(".norm.linear") or module == "norm_out.linear":
+        return 1
+    if module.startswith("single_transformer_blocks."):
+        return L + N
+    if module == "context_embedder" or ".add_" in module or ".to_add_out" in module or ".ff_context." in module:
+        return L
+    return N
+
+
+def lora_macs_per_image(wrapper, L: int, N: int) -> float:
+    """algorithmic forward MACs of the LoRA branches: rows x r x (cin + cout) per adapted module."""
+    macs = 0.0
+    for s in wrapper.sites:
+        for m, co in zip(s.modules, s.couts_ref):
+            macs += rows_per_image(m, L, N) * wrapper.rank * (s.cin_ref + co)
+    return macs
