@@ -95,12 +95,16 @@ def gemm_roofline(tr, batch):
         e1.record()
         recs.append((2.0 * a.M * a.N * a.K, e0, e1))
 
+    from onetrainer_amd.module import streams
+    was = streams.enabled()
+    streams.set_enabled(False)   # per-launch durations in isolation (no side-stream overlap)
     K._gemm = timed
     try:
         tr.train_step(batch)
         torch.cuda.synchronize()
     finally:
         K._gemm = orig
+        streams.set_enabled(was)
     flops = sum(r[0] for r in recs)
     ms = sum(r[1].elapsed_time(r[2]) for r in recs)
     return flops, ms, len(recs)

@@ -39,11 +39,15 @@ _WS: dict[int, torch.Tensor] = {}
 
 
 def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
+    """scratch for the launch about to be queued on the current stream: one buffer per
+    (device, stream), so work on the weight-gradient side stream (module/streams.py) never shares
+    split-K slabs with the main stream.  Reuse is stream-ordered."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    ws = _WS.get(idx)
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
+    ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(max(nbytes, 64 << 20), dtype=torch.uint8, device=device)
-        _WS[idx] = ws
+        _WS[key] = ws
     return ws
 
 

@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 
 from .. import kernels as K
+from . import streams as S
 from .functional import _trainable_params
 
 
@@ -72,23 +73,31 @@ class RowsLinearFn(torch.autograd.Function):
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         for (r0, r1, wref, bref, site), t in zip(ctx.segs, ctx.ts):
             dys, xs = dy[r0:r1], x[r0:r1]
-            if site is not None:
-                u = K.linear_dgrad(dys, site.up2)
-                if dx is not None:
+            btr = bref is not None and bref.trainable
+            u = K.linear_dgrad(dys, site.up2) if site is not None else None
+            if site is not None or wref.trainable or btr:
+                with S.wgrad_region((dys, xs, t, u)):
+                    if site is not None:
+                        acc = site.acc()
+                        K.linear_wgrad(u, xs, out=site.g_down, accumulate=acc)
+                        rk = site.rank
+                        for p, (g, (n0, n1)) in enumerate(zip(site.g_up, site.ranges)):
+                            K.linear_wgrad(dys[:, n0:n1], t[:, p * rk:(p + 1) * rk], out=g, accumulate=acc,
+                                           alpha=site.scale)
+                    if wref.trainable:
+                        K.linear_wgrad(dys, xs, out=wref.g, accumulate=wref.acc())
+                    if btr:
+                        K.colsum(dys, out=bref.g.view(1, -1), accumulate=bref.acc())
+            if dx is not None:
+                if site is not None:
                     K.linear_dgrad(dys, wref.w, lora=(u, site.down), out=dx[r0:r1])
-                acc = site.acc()
-                K.linear_wgrad(u, xs, out=site.g_down, accumulate=acc)
-                rk = site.rank
-                for p, (g, (n0, n1)) in enumerate(zip(site.g_up, site.ranges)):
-                    K.linear_wgrad(dys[:, n0:n1], t[:, p * rk:(p + 1) * rk], out=g, accumulate=acc, alpha=site.scale)
+                else:
+                    K.linear_dgrad(dys, wref.w, out=dx[r0:r1])
+            if site is not None:
                 site.done()
-            elif dx is not None:
-                K.linear_dgrad(dys, wref.w, out=dx[r0:r1])
             if wref.trainable:
-                K.linear_wgrad(dys, xs, out=wref.g, accumulate=wref.acc())
                 wref.done()
-            if bref is not None and bref.trainable:
-                K.colsum(dys, out=bref.g.view(1, -1), accumulate=bref.acc())
+            if btr:
                 bref.done()
         return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 

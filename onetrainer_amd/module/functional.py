@@ -13,6 +13,7 @@ from __future__ import annotations
 import torch
 
 from .. import kernels as K
+from . import streams as S
 
 
 class PRef:
@@ -80,14 +81,19 @@ class LinearFn(torch.autograd.Function):
         dy2 = _rows(dy)
         if dy2.stride(1) != 1 or dy2.stride(0) % 8:
             dy2 = dy2.contiguous()
+        btr = bref is not None and bref.trainable
+        if wref.trainable or btr:
+            with S.wgrad_region((dy2, x2)):       # weight gradients overlap the dgrad chain
+                if wref.trainable:
+                    K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
+                if btr:
+                    K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.linear_dgrad(dy2, wref.w).view(ctx.xshape)
         if wref.trainable:
-            K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
             wref.done()
-        if bref is not None and bref.trainable:
-            K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
+        if btr:
             bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, dres) + (None,) * (len(ctx.needs_input_grad) - 4)
@@ -128,20 +134,24 @@ class LoraLinearFn(torch.autograd.Function):
         if dy2.stride(1) != 1 or dy2.stride(0) % 8:
             dy2 = dy2.contiguous()
         u = K.linear_dgrad(dy2, site.up2)
+        btr = bref is not None and bref.trainable
+        with S.wgrad_region((dy2, x2, t, u)):
+            acc = site.acc()
+            K.linear_wgrad(u, x2, out=site.g_down, accumulate=acc)
+            r = site.rank
+            for p, (g, (n0, n1)) in enumerate(zip(site.g_up, site.ranges)):
+                K.linear_wgrad(dy2[:, n0:n1], t[:, p * r:(p + 1) * r], out=g, accumulate=acc, alpha=site.scale)
+            if wref.trainable:
+                K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
+            if btr:
+                K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.linear_dgrad(dy2, wref.w, lora=(u, site.down)).view(ctx.xshape)
-        acc = site.acc()
-        K.linear_wgrad(u, x2, out=site.g_down, accumulate=acc)
-        r = site.rank
-        for p, (g, (n0, n1)) in enumerate(zip(site.g_up, site.ranges)):
-            K.linear_wgrad(dy2[:, n0:n1], t[:, p * r:(p + 1) * r], out=g, accumulate=acc, alpha=site.scale)
         site.done()
         if wref.trainable:
-            K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
             wref.done()
-        if bref is not None and bref.trainable:
-            K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
+        if btr:
             bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, dres, None) + (None,) * (len(ctx.needs_input_grad) - 5)
@@ -168,6 +178,13 @@ class ConvFn(torch.autograd.Function):
                 or dy.stride(0) != dy.stride(1) * dy.shape[1]:
             dy = dy.contiguous()
         N, H, W, _ = x.shape
+        btr = bref is not None and bref.trainable
+        if wref.trainable or btr:
+            with S.wgrad_region((dy, x)):
+                if wref.trainable:
+                    K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
+                if btr:
+                    K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.upsample:
@@ -175,16 +192,14 @@ class ConvFn(torch.autograd.Function):
                 dx = K.upsample2x_bwd(dup)
             else:
                 dx = K.conv2d_dgrad(dy, wref.w, (H, W), ctx.stride, 1)
-        if wref.trainable:
-            K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
-            wref.done()
         drow = None
         P, Q = dy.shape[1], dy.shape[2]
         if ctx.has_rowvec:
             drow = K.colsum(dy, rows_per_group=P * Q, out=torch.empty((dy.shape[0], dy.shape[3]), dtype=torch.bfloat16,
                                                                        device=dy.device))
-        if bref is not None and bref.trainable:
-            K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
+        if wref.trainable:
+            wref.done()
+        if btr:
             bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, drow, dres, None, None) + (None,) * (len(ctx.needs_input_grad) - 7)
@@ -217,6 +232,15 @@ class LoraConvFn(torch.autograd.Function):
         dy2 = dy.reshape(M, Cout)
         r = site.rank
         u = K.linear_dgrad(dy2, site.up2).view(N, P, Q, r)          # dy (s B)
+        btr = bref is not None and bref.trainable
+        with S.wgrad_region((dy, x, t, u)):
+            acc = site.acc()
+            K.conv2d_wgrad(u, x, site.k, ctx.stride, 1, upsample=ctx.upsample, out=site.g_down, accumulate=acc)
+            K.linear_wgrad(dy2, t.reshape(M, r), out=site.g_up[0], accumulate=acc, alpha=site.scale)
+            if wref.trainable:
+                K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
+            if btr:
+                K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.upsample:
@@ -226,18 +250,13 @@ class LoraConvFn(torch.autograd.Function):
             else:
                 dx = K.conv2d_dgrad(dy, wref.w, (H, W), ctx.stride, 1)
                 K.conv2d_dgrad(u, site.down, (H, W), ctx.stride, 1, out=dx, accumulate=True)
-        acc = site.acc()
-        K.conv2d_wgrad(u, x, site.k, ctx.stride, 1, upsample=ctx.upsample, out=site.g_down, accumulate=acc)
-        K.linear_wgrad(dy2, t.reshape(M, r), out=site.g_up[0], accumulate=acc, alpha=site.scale)
         site.done()
-        if wref.trainable:
-            K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
-            wref.done()
         drow = None
         if ctx.has_rowvec:
             drow = K.colsum(dy, rows_per_group=P * Q, out=torch.empty((N, Cout), dtype=torch.bfloat16, device=dy.device))
-        if bref is not None and bref.trainable:
-            K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
+        if wref.trainable:
+            wref.done()
+        if btr:
             bref.done()
         dres = dy if ctx.has_res else None
         return (dx, None, None, drow, dres, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 8)

@@ -101,7 +101,11 @@ class FlatParamStore:
         self._written.clear()
 
     def finish_backward(self):
-        """zero the grads of parameters that received none this micro-step (overwrite semantics)."""
+        """join the weight-gradient stream, then zero the grads of parameters that received none
+        this micro-step (overwrite semantics)."""
+        if self.device.type == "cuda":
+            from .streams import join
+            join()
         if self.trainable and not self.accumulating:
             for n in self.order:
                 if n not in self._written:

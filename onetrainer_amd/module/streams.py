@@ -1,0 +1,80 @@
+"""Side HIP stream for weight-gradient work (MI355X-first scheduling, no reference counterpart).
+
+In backward every Linear / conv needs dgrad (on the critical path: the next layer's backward
+waits for it) and wgrad + bias colsum (needed only by the optimizer / DP all-reduce).  At b = 4
+many of these GEMMs fill only part of the 256 CUs (e.g. 4096 x 1280 x 1280: 160 tiles of
+256 x 128), so running the weight-gradient GEMMs on a second stream lets them occupy the CUs the
+dgrad chain leaves idle instead of serialising behind it.
+
+    with wgrad_region(tensors):   # side stream waits for everything queued on the main stream so
+        ...launch wgrad...        # far (dy, x ready), kernels go to the side stream; the tensors
+                                  # are record_stream()ed so the caching allocator cannot recycle
+                                  # them before the side stream has read them
+    join()                        # main stream waits for the side stream (before clip / AdamW)
+
+OTAMD_WGRAD_STREAM=0 disables it (everything on the current stream).  The GEMM workspace is
+per stream (kernels.workspace), so the two streams never share split-K slabs.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+
+import torch
+
+_SIDE: dict = {}
+_ENABLED = os.environ.get("OTAMD_WGRAD_STREAM", "1") != "0"
+
+
+def enabled() -> bool:
+    return _ENABLED and torch.cuda.is_available()
+
+
+def set_enabled(on: bool):
+    global _ENABLED
+    _ENABLED = bool(on)
+
+
+def side_stream(device=None):
+    if not enabled():
+        return None
+    idx = torch.cuda.current_device() if device is None else torch.device(device).index
+    if idx is None:
+        idx = torch.cuda.current_device()
+    s = _SIDE.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _SIDE[idx] = s
+    return s
+
+
+@contextlib.contextmanager
+def wgrad_region(tensors=()):
+    side = side_stream()
+    if side is None:
+        yield
+        return
+    main = torch.cuda.current_stream()
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        yield
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(side)
+
+
+def join():
+    """make the current stream wait for all weight-gradient work queued so far."""
+    side = side_stream()
+    if side is not None:
+        torch.cuda.current_stream().wait_stream(side)
+
+
+def after_side(fn):
+    """run fn (e.g. an async all-reduce launch) ordered after both streams' work so far."""
+    side = side_stream()
+    if side is None:
+        return fn()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        return fn()

@@ -16,6 +16,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ..module.streams import after_side
+
 
 class GradBucketReducer:
     def __init__(self, store, group=None, bucket_bytes: int = 256 << 20):
@@ -54,16 +56,19 @@ class GradBucketReducer:
             self.pending[bi] -= 1
             if self.pending[bi] == 0:
                 b, e, _ = self.buckets[bi]
-                self.works.append(dist.all_reduce(self.store.grad[b:e], op=dist.ReduceOp.SUM, group=self.group,
-                                                  async_op=True))
+                g = self.store.grad[b:e]
+                # ordered after both the main stream and the weight-gradient stream (module/streams.py)
+                self.works.append(after_side(lambda: dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
+                                                                     async_op=True)))
 
     def finish(self):
         """reduce any bucket not yet launched (unused params), then wait for all of them."""
         for bi, cnt in enumerate(self.pending):
             if cnt > 0:
                 b, e, _ = self.buckets[bi]
-                self.works.append(dist.all_reduce(self.store.grad[b:e], op=dist.ReduceOp.SUM, group=self.group,
-                                                  async_op=True))
+                g = self.store.grad[b:e]
+                self.works.append(after_side(lambda: dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
+                                                                     async_op=True)))
         for w in self.works:
             w.wait()
         self.works = []
