@@ -172,14 +172,17 @@ int otamd_flux_pack(const void* src, void* dst, int B, int h, int w, int C, int 
 
 /* replaces: ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out (diffusers, via BaseStableDiffusionXLSetup.py:268-273) */
 int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long long ldy, int N, int HW, int C, int G,
-    float eps, const void* gamma, const void* beta, int silu, float* mean, float* rstd, float* a, float* b,
-    double* ws, hipStream_t stream);
+                        float eps, const void* gamma, const void* beta, int silu, float* mean, float* rstd, float* a,
+                        float* b, float* ws, hipStream_t stream);
 
 /* replaces: autograd of GroupNorm(+SiLU) */
-int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long
-    lddx, int N, int HW, int C, int G, const void* gamma, int silu, const float* mean, const float* rstd,
-    const float* a, const float* b, void* dgamma, void* dbeta, int param_f32, int param_acc, double* ws,
-    float* fws, int accumulate, hipStream_t stream);
+int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long lddx,
+                        int N, int HW, int C, int G, const void* gamma, int silu, const float* mean, const float* rstd,
+                        const float* a, const float* b, void* dgamma, void* dbeta, int param_f32, int param_acc,
+                        float* ws, int accumulate, hipStream_t stream);
+
+/* scratch floats otamd_groupnorm_fwd / _bwd need for these sizes (partial slabs, coefficients, sums) */
+long long otamd_groupnorm_ws_floats(int N, int HW, int C);
 
 /* replaces: BasicTransformerBlock norm1/norm2/norm3 */
 int otamd_layernorm_fwd(const void* x, long long ldx, void* y, long long ldy, int rows, int C, float eps,

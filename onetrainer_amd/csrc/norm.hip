@@ -15,291 +15,397 @@
 __device__ __forceinline__ void store_param_grad(void* p, long long i, float v, int f32, int acc);
 
 // ------------------------------------------------------------------------------------------
-// per-(n, c) partial sums of x and x^2, accumulated in double via atomics
-// grid: (pixel blocks, N); block 256 threads; thread t owns channel chunk t % C8 and pixels
-// p = t / C8 + k * (256 / C8)
-__global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, long long ldx, int HW, int C,
-                                                       int pix_per_block, double* __restrict__ sum,
-                                                       double* __restrict__ sumsq) {
-  extern __shared__ float sred[];   // [2][C]
+// Pixel-loop structure (all four passes): a block of C8 * PPP threads (PPP = max(1, 256 / C8)
+// pixels per pass) gives each thread ONE fixed 8-channel chunk, so its per-channel constants
+// live in registers and every load is a 16-byte chunk; the thread walks pixels p = p0 + lane_pix,
+// p0 + lane_pix + PPP, ... of the block's pixel range, 4 pixels per iteration in flight.
+// Reductions write per-block partial slabs (no atomics, deterministic); a finalize kernel folds
+// blocks and channels into the (n, group) constants.
+static inline int gn_threads(int C8) { return C8 * (C8 >= 256 ? 1 : 256 / C8); }
+
+__device__ __forceinline__ void gn_coef8(const float* __restrict__ p, float (&v)[8]) {
+  const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w; v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+}
+
+// fwd pass 1: part[blk][0|1][c] = sum x, sum x^2 over the block's pixels of image n = blockIdx.y
+__global__ void __launch_bounds__(512) gn_stats_kernel(const bf16_t* __restrict__ x, long long ldx, int HW, int C,
+                                                       int pix_per_block, float* __restrict__ part) {
+  extern __shared__ float sred[];   // [PPP][2][C]
   const int n = blockIdx.y;
   const int C8 = C >> 3;
-  const int lanes_per_pix = C8 <= 256 ? C8 : 256;
-  const int pix_stride = 256 / lanes_per_pix;
-  const int t = threadIdx.x;
-  for (int i = t; i < 2 * C; i += 256) sred[i] = 0.f;
-  __syncthreads();
-  const int p0 = blockIdx.x * pix_per_block;
-  const int p1 = min(HW, p0 + pix_per_block);
-  if (t < lanes_per_pix * pix_stride) {
-    for (int c8 = t % lanes_per_pix; c8 < C8; c8 += lanes_per_pix) {
-      float s[8] = {0}, q[8] = {0};
-      for (int p = p0 + t / lanes_per_pix; p < p1; p += pix_stride) {
-        bf8 v = *reinterpret_cast<const bf8*>(x + ((long long)n * HW + p) * ldx + c8 * 8);
-        float f[8];
-        unpack8(v, f);
+  const int PPP = blockDim.x / C8;
+  const int t = threadIdx.x, c8 = t % C8, lp = t / C8;
+  const int p0 = blockIdx.x * pix_per_block, p1 = min(HW, p0 + pix_per_block);
+  const bf16_t* xb = x + (long long)n * HW * ldx + c8 * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int p = p0 + lp;
+  for (; p + 3 * PPP < p1; p += 4 * PPP) {
+    bf8 v[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
-      }
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const bf8*>(xb + (long long)(p + u * PPP) * ldx);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        atomicAdd(&sred[c8 * 8 + j], s[j]);
-        atomicAdd(&sred[C + c8 * 8 + j], q[j]);
-      }
+    for (int u = 0; u < 4; ++u) {
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
     }
   }
+  for (; p < p1; p += PPP) {
+    float f[8];
+    unpack8(*reinterpret_cast<const bf8*>(xb + (long long)p * ldx), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sred[(lp * 2) * C + c8 * 8 + j] = s[j]; sred[(lp * 2 + 1) * C + c8 * 8 + j] = q[j]; }
   __syncthreads();
-  for (int c = t; c < C; c += 256) {
-    atomicAdd(&sum[(long long)n * C + c], (double)sred[c]);
-    atomicAdd(&sumsq[(long long)n * C + c], (double)sred[C + c]);
+  float* dst = part + ((long long)n * gridDim.x + blockIdx.x) * 2 * C;
+  for (int i = t; i < 2 * C; i += blockDim.x) {
+    const int w = i / C, c = i - w * C;
+    float acc = 0.f;
+    for (int k = 0; k < PPP; ++k) acc += sred[(k * 2 + w) * C + c];
+    dst[i] = acc;
   }
 }
 
-// fold channel sums into groups; emit per-(n,c) affine a = rstd*gamma, b = beta - mean*a,
-// and per-(n,g) mean / rstd for the backward.  grid N, block 256
-__global__ void gn_finalize_kernel(const double* __restrict__ sum, const double* __restrict__ sumsq, int HW, int C,
-                                   int G, float eps, const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+// sum the per-block partial slabs over blocks in double: out[n][i] = sum_blk part[n][blk][i], i < 2C.
+// grid (ceil(2C / 64), N), block 1024 = 64 columns x 16 partial lanes (coalesced column reads)
+__global__ void __launch_bounds__(1024) gn_colreduce_kernel(const float* __restrict__ part, int nblk, int C2,
+                                                            double* __restrict__ out) {
+  __shared__ double red[16][65];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int n = blockIdx.y, i = blockIdx.x * 64 + cl;
+  double s = 0.0;
+  if (i < C2) {
+    const float* pb = part + (long long)n * nblk * C2 + i;
+    for (int blk = pl; blk < nblk; blk += 16) s += pb[(long long)blk * C2];
+  }
+  red[pl][cl] = s;
+  __syncthreads();
+  if (pl == 0 && i < C2) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    out[(long long)n * C2 + i] = t;
+  }
+}
+
+// fold channel sums into groups: mean / rstd per (n, g); a = rstd*gamma, b = beta - mean*a per (n, c).
+// sums: [N][2][C] double (sum x, sum x^2).  grid N, block 256
+__global__ void gn_finalize_kernel(const double* __restrict__ sums, int HW, int C, int G, float eps,
+                                   const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
                                    float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ a_out,
                                    float* __restrict__ b_out) {
   const int n = blockIdx.x;
   const int Cg = C / G;
+  const double* s = sums + (long long)n * 2 * C;
   for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    double s = 0, q = 0;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { s += sum[(long long)n * C + c]; q += sumsq[(long long)n * C + c]; }
+    double sm = 0, sq = 0;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { sm += s[c]; sq += s[C + c]; }
     const double cnt = (double)HW * Cg;
-    const double mean = s / cnt;
-    double var = q / cnt - mean * mean;
+    const double mean = sm / cnt;
+    double var = sq / cnt - mean * mean;
     if (var < 0) var = 0;
-    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
     mean_out[n * G + g] = (float)mean;
-    rstd_out[n * G + g] = rstd;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      const float gm = gamma ? bf2f(gamma[c]) : 1.f;
-      const float bt = beta ? bf2f(beta[c]) : 0.f;
-      const float a = rstd * gm;
-      a_out[n * C + c] = a;
-      b_out[n * C + c] = bt - (float)mean * a;
-    }
+    rstd_out[n * G + g] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / Cg;
+    const float m = mean_out[n * G + g], r = rstd_out[n * G + g];
+    const float gm = gamma ? bf2f(gamma[c]) : 1.f;
+    const float bt = beta ? bf2f(beta[c]) : 0.f;
+    const float av = r * gm;
+    a_out[n * C + c] = av;
+    b_out[n * C + c] = bt - m * av;
   }
 }
 
-// y = [silu](x * a[n,c] + b[n,c]); grid-stride over 16-byte chunks
+// y = [silu](x * a[n,c] + b[n,c])
 template <bool SILU>
-__global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, long long ldx, bf16_t* __restrict__ y,
-                                                       long long ldy, int N, int HW, int C, const float* __restrict__ a,
-                                                       const float* __restrict__ b) {
+__global__ void __launch_bounds__(512) gn_apply_kernel(const bf16_t* __restrict__ x, long long ldx, bf16_t* __restrict__ y,
+                                                       long long ldy, int HW, int C, int pix_per_block,
+                                                       const float* __restrict__ a, const float* __restrict__ b) {
+  const int n = blockIdx.y;
   const int C8 = C >> 3;
-  const long long total = (long long)N * HW * C8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const long long pix = i / C8;
-    const int c0 = (int)(i - pix * C8) * 8;
-    const int n = (int)(pix / HW);
-    bf8 v = *reinterpret_cast<const bf8*>(x + pix * ldx + c0);
-    float f[8];
-    unpack8(v, f);
-    const float4 a0 = *reinterpret_cast<const float4*>(a + (long long)n * C + c0);
-    const float4 a1 = *reinterpret_cast<const float4*>(a + (long long)n * C + c0 + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(b + (long long)n * C + c0);
-    const float4 b1 = *reinterpret_cast<const float4*>(b + (long long)n * C + c0 + 4);
-    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  const int PPP = blockDim.x / C8;
+  const int t = threadIdx.x, c8 = t % C8, lp = t / C8;
+  float av[8], bv[8];
+  gn_coef8(a + (long long)n * C + c8 * 8, av);
+  gn_coef8(b + (long long)n * C + c8 * 8, bv);
+  const int p0 = blockIdx.x * pix_per_block, p1 = min(HW, p0 + pix_per_block);
+  const bf16_t* xb = x + (long long)n * HW * ldx + c8 * 8;
+  bf16_t* yb = y + (long long)n * HW * ldy + c8 * 8;
+  int p = p0 + lp;
+  for (; p + 3 * PPP < p1; p += 4 * PPP) {
+    bf8 v[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float z = fmaf(f[j], av[j], bv[j]);
-      f[j] = SILU ? silu_f(z) : z;
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const bf8*>(xb + (long long)(p + u * PPP) * ldx);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float z = fmaf(f[j], av[j], bv[j]); f[j] = SILU ? silu_f(z) : z; }
+      *reinterpret_cast<bf8*>(yb + (long long)(p + u * PPP) * ldy) = pack8(f);
     }
-    *reinterpret_cast<bf8*>(y + pix * ldy + c0) = pack8(f);
+  }
+  for (; p < p1; p += PPP) {
+    float f[8];
+    unpack8(*reinterpret_cast<const bf8*>(xb + (long long)p * ldx), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float z = fmaf(f[j], av[j], bv[j]); f[j] = SILU ? silu_f(z) : z; }
+    *reinterpret_cast<bf8*>(yb + (long long)p * ldy) = pack8(f);
   }
 }
 
-// backward pass 1: per-(n,c) S1 = sum dz, S2 = sum dz * xhat   (dz = dy * silu'(z) when SILU)
+// backward pass 1: part[blk][0|1][c] = sum dz, sum dz * xhat   (dz = dy * silu'(z) when SILU)
 template <bool SILU>
-__global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const bf16_t* __restrict__ x, long long ldx,
+__global__ void __launch_bounds__(512) gn_bwd_reduce_kernel(const bf16_t* __restrict__ x, long long ldx,
                                                             const bf16_t* __restrict__ dy, long long lddy, int HW, int C,
                                                             int G, int pix_per_block, const float* __restrict__ a,
                                                             const float* __restrict__ b, const float* __restrict__ mean,
-                                                            const float* __restrict__ rstd, double* __restrict__ s1,
-                                                            double* __restrict__ s2) {
-  extern __shared__ float sred[];   // [2][C]
+                                                            const float* __restrict__ rstd, float* __restrict__ part) {
+  extern __shared__ float sred[];   // [PPP][2][C]
   const int n = blockIdx.y;
   const int C8 = C >> 3;
+  const int PPP = blockDim.x / C8;
   const int Cg = C / G;
-  const int lanes_per_pix = C8 <= 256 ? C8 : 256;
-  const int pix_stride = 256 / lanes_per_pix;
-  const int t = threadIdx.x;
-  for (int i = t; i < 2 * C; i += 256) sred[i] = 0.f;
-  __syncthreads();
-  const int p0 = blockIdx.x * pix_per_block;
-  const int p1 = min(HW, p0 + pix_per_block);
-  if (t < lanes_per_pix * pix_stride) {
-    for (int c8 = t % lanes_per_pix; c8 < C8; c8 += lanes_per_pix) {
-      const int c0 = c8 * 8;
-      float av[8], bv[8], mv[8], rv[8];
+  const int t = threadIdx.x, c8 = t % C8, lp = t / C8;
+  float av[8], bv[8], mv[8], rv[8];
+  gn_coef8(a + (long long)n * C + c8 * 8, av);
+  gn_coef8(b + (long long)n * C + c8 * 8, bv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        av[j] = a[(long long)n * C + c0 + j];
-        bv[j] = b[(long long)n * C + c0 + j];
-        const int g = (c0 + j) / Cg;
-        mv[j] = mean[n * G + g];
-        rv[j] = rstd[n * G + g];
-      }
-      float s[8] = {0}, q[8] = {0};
-      for (int p = p0 + t / lanes_per_pix; p < p1; p += pix_stride) {
-        const long long pix = (long long)n * HW + p;
-        bf8 xv = *reinterpret_cast<const bf8*>(x + pix * ldx + c0);
-        bf8 gv = *reinterpret_cast<const bf8*>(dy + pix * lddy + c0);
-        float xf[8], gf[8];
-        unpack8(xv, xf);
-        unpack8(gv, gf);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float dz = gf[j];
-          if (SILU) dz *= dsilu_f(fmaf(xf[j], av[j], bv[j]));
-          const float xh = (xf[j] - mv[j]) * rv[j];
-          s[j] += dz;
-          q[j] = fmaf(dz, xh, q[j]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        atomicAdd(&sred[c0 + j], s[j]);
-        atomicAdd(&sred[C + c0 + j], q[j]);
-      }
-    }
+  for (int j = 0; j < 8; ++j) {
+    const int g = (c8 * 8 + j) / Cg;
+    mv[j] = mean[n * G + g];
+    rv[j] = rstd[n * G + g];
   }
+  const int p0 = blockIdx.x * pix_per_block, p1 = min(HW, p0 + pix_per_block);
+  const bf16_t* xb = x + (long long)n * HW * ldx + c8 * 8;
+  const bf16_t* gb = dy + (long long)n * HW * lddy + c8 * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto body = [&](const bf8& xv, const bf8& gv) {
+    float xf[8], gf[8];
+    unpack8(xv, xf);
+    unpack8(gv, gf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float dz = gf[j];
+      if (SILU) dz *= dsilu_f(fmaf(xf[j], av[j], bv[j]));
+      s[j] += dz;
+      q[j] = fmaf(dz, (xf[j] - mv[j]) * rv[j], q[j]);
+    }
+  };
+  int p = p0 + lp;
+  for (; p + PPP < p1; p += 2 * PPP) {
+    const bf8 x0 = *reinterpret_cast<const bf8*>(xb + (long long)p * ldx);
+    const bf8 g0 = *reinterpret_cast<const bf8*>(gb + (long long)p * lddy);
+    const bf8 x1 = *reinterpret_cast<const bf8*>(xb + (long long)(p + PPP) * ldx);
+    const bf8 g1 = *reinterpret_cast<const bf8*>(gb + (long long)(p + PPP) * lddy);
+    body(x0, g0);
+    body(x1, g1);
+  }
+  for (; p < p1; p += PPP)
+    body(*reinterpret_cast<const bf8*>(xb + (long long)p * ldx), *reinterpret_cast<const bf8*>(gb + (long long)p * lddy));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sred[(lp * 2) * C + c8 * 8 + j] = s[j]; sred[(lp * 2 + 1) * C + c8 * 8 + j] = q[j]; }
   __syncthreads();
-  for (int c = t; c < C; c += 256) {
-    atomicAdd(&s1[(long long)n * C + c], (double)sred[c]);
-    atomicAdd(&s2[(long long)n * C + c], (double)sred[C + c]);
+  float* dst = part + ((long long)n * gridDim.x + blockIdx.x) * 2 * C;
+  for (int i = t; i < 2 * C; i += blockDim.x) {
+    const int w = i / C, c = i - w * C;
+    float acc = 0.f;
+    for (int k = 0; k < PPP; ++k) acc += sred[(k * 2 + w) * C + c];
+    dst[i] = acc;
   }
 }
 
-// per-(n,g) constants c1 = sum_c gamma_c S1 / cnt, c2 = sum_c gamma_c S2 / cnt; also dgamma/dbeta
-__global__ void gn_bwd_finalize_kernel(const double* __restrict__ s1, const double* __restrict__ s2, int N, int HW,
-                                       int C, int G, const bf16_t* __restrict__ gamma, float* __restrict__ c1,
-                                       float* __restrict__ c2, void* __restrict__ dgamma, void* __restrict__ dbeta,
-                                       int pf32, int pacc) {
+// per (n, g) c1 = sum_c gamma S1 / cnt, c2 = sum_c gamma S2 / cnt from the block-summed
+// sums [N][2][C] (S1 = sum dz, S2 = sum dz xhat), folded into the apply coefficients
+// dx = A dz + B x + Cc with A = rstd gamma, B = -rstd^2 c2, Cc = rstd (mean rstd c2 - c1).
+// coef: [3][N][C] fp32.  grid N, block 256
+__global__ void gn_bwd_finalize_kernel(const double* __restrict__ sums, int N, int HW, int C, int G,
+                                       const bf16_t* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ rstd, float* __restrict__ coef) {
+  __shared__ float cc[2][256];
+  const int n = blockIdx.x;
   const int Cg = C / G;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N * G; i += gridDim.x * blockDim.x) {
-    const int n = i / G, g = i - n * G;
-    double a = 0, bsum = 0;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      const double gm = gamma ? bf2f(gamma[c]) : 1.0;
-      a += gm * s1[(long long)n * C + c];
-      bsum += gm * s2[(long long)n * C + c];
+  const double* s1 = sums + (long long)n * 2 * C;
+  const double* s2 = s1 + C;
+  for (int g0 = 0; g0 < G; g0 += 256) {
+    const int g = g0 + threadIdx.x;
+    if (g < G) {
+      double a = 0, q = 0;
+      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+        const double gm = gamma ? bf2f(gamma[c]) : 1.0;
+        a += gm * s1[c];
+        q += gm * s2[c];
+      }
+      cc[0][threadIdx.x] = (float)(a / ((double)HW * Cg));
+      cc[1][threadIdx.x] = (float)(q / ((double)HW * Cg));
     }
-    const double cnt = (double)HW * Cg;
-    c1[i] = (float)(a / cnt);
-    c2[i] = (float)(bsum / cnt);
+    __syncthreads();
+    for (int c = g0 * Cg + threadIdx.x; c < min(G, g0 + 256) * Cg; c += blockDim.x) {
+      const int gi = c / Cg - g0, ng = n * G + g0 + gi;
+      const float r = rstd[ng], m = mean[ng];
+      const float c1 = cc[0][gi], c2 = cc[1][gi];
+      const float gm = gamma ? bf2f(gamma[c]) : 1.f;
+      coef[(long long)n * C + c] = r * gm;
+      coef[(long long)(N + n) * C + c] = -r * r * c2;
+      coef[(long long)(2 * N + n) * C + c] = r * (m * r * c2 - c1);
+    }
+    __syncthreads();
   }
+}
+
+// dgamma[c] = sum_n S2[n][c], dbeta[c] = sum_n S1[n][c]
+__global__ void gn_param_grad_kernel(const double* __restrict__ sums, int N, int C, void* __restrict__ dgamma,
+                                     void* __restrict__ dbeta, int pf32, int pacc) {
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     double dg = 0, db = 0;
-    for (int n = 0; n < N; ++n) { dg += s2[(long long)n * C + c]; db += s1[(long long)n * C + c]; }
+    for (int n = 0; n < N; ++n) { db += sums[(long long)n * 2 * C + c]; dg += sums[(long long)n * 2 * C + C + c]; }
     if (dgamma) store_param_grad(dgamma, c, (float)dg, pf32, pacc);
     if (dbeta) store_param_grad(dbeta, c, (float)db, pf32, pacc);
   }
 }
 
-// dx = rstd * (dz*gamma - c1 - xhat*c2)
+// dx = A dz + B x + Cc  (dz = dy * silu'(x a + b) when SILU)
 template <bool SILU>
-__global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const bf16_t* __restrict__ x, long long ldx,
+__global__ void __launch_bounds__(512) gn_bwd_apply_kernel(const bf16_t* __restrict__ x, long long ldx,
                                                            const bf16_t* __restrict__ dy, long long lddy,
                                                            bf16_t* __restrict__ dx, long long lddx, int N, int HW, int C,
-                                                           int G, const bf16_t* __restrict__ gamma,
-                                                           const float* __restrict__ a, const float* __restrict__ b,
-                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                           const float* __restrict__ c1, const float* __restrict__ c2,
+                                                           int pix_per_block, const float* __restrict__ a,
+                                                           const float* __restrict__ b, const float* __restrict__ coef,
                                                            int accumulate) {
+  const int n = blockIdx.y;
   const int C8 = C >> 3;
-  const int Cg = C / G;
-  const long long total = (long long)N * HW * C8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const long long pix = i / C8;
-    const int c0 = (int)(i - pix * C8) * 8;
-    const int n = (int)(pix / HW);
-    bf8 xv = *reinterpret_cast<const bf8*>(x + pix * ldx + c0);
-    bf8 gv = *reinterpret_cast<const bf8*>(dy + pix * lddy + c0);
+  const int PPP = blockDim.x / C8;
+  const int t = threadIdx.x, c8 = t % C8, lp = t / C8;
+  float av[8], bv[8], A[8], Bv[8], Cc[8];
+  gn_coef8(coef + (long long)n * C + c8 * 8, A);
+  gn_coef8(coef + (long long)(N + n) * C + c8 * 8, Bv);
+  gn_coef8(coef + (long long)(2 * N + n) * C + c8 * 8, Cc);
+  if (SILU) {
+    gn_coef8(a + (long long)n * C + c8 * 8, av);
+    gn_coef8(b + (long long)n * C + c8 * 8, bv);
+  }
+  const int p0 = blockIdx.x * pix_per_block, p1 = min(HW, p0 + pix_per_block);
+  const bf16_t* xb = x + (long long)n * HW * ldx + c8 * 8;
+  const bf16_t* gb = dy + (long long)n * HW * lddy + c8 * 8;
+  bf16_t* ob = dx + (long long)n * HW * lddx + c8 * 8;
+  auto body = [&](int pp, const bf8& xv, const bf8& gv) {
     float xf[8], gf[8], o[8];
     unpack8(xv, xf);
     unpack8(gv, gf);
     float prev[8];
-    if (accumulate) { bf8 pv = *reinterpret_cast<const bf8*>(dx + pix * lddx + c0); unpack8(pv, prev); }
+    if (accumulate) unpack8(*reinterpret_cast<const bf8*>(ob + (long long)pp * lddx), prev);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j, g = c / Cg, ng = n * G + g;
       float dz = gf[j];
-      if (SILU) dz *= dsilu_f(fmaf(xf[j], a[(long long)n * C + c], b[(long long)n * C + c]));
-      const float r = rstd[ng];
-      const float xh = (xf[j] - mean[ng]) * r;
-      const float gm = gamma ? bf2f(gamma[c]) : 1.f;
-      o[j] = r * (dz * gm - c1[ng] - xh * c2[ng]);
+      if (SILU) dz *= dsilu_f(fmaf(xf[j], av[j], bv[j]));
+      o[j] = fmaf(A[j], dz, fmaf(Bv[j], xf[j], Cc[j]));
       if (accumulate) o[j] += prev[j];
     }
-    *reinterpret_cast<bf8*>(dx + pix * lddx + c0) = pack8(o);
+    *reinterpret_cast<bf8*>(ob + (long long)pp * lddx) = pack8(o);
+  };
+  int p = p0 + lp;
+  for (; p + PPP < p1; p += 2 * PPP) {
+    const bf8 x0 = *reinterpret_cast<const bf8*>(xb + (long long)p * ldx);
+    const bf8 g0 = *reinterpret_cast<const bf8*>(gb + (long long)p * lddy);
+    const bf8 x1 = *reinterpret_cast<const bf8*>(xb + (long long)(p + PPP) * ldx);
+    const bf8 g1 = *reinterpret_cast<const bf8*>(gb + (long long)(p + PPP) * lddy);
+    body(p, x0, g0);
+    body(p + PPP, x1, g1);
   }
+  for (; p < p1; p += PPP)
+    body(p, *reinterpret_cast<const bf8*>(xb + (long long)p * ldx), *reinterpret_cast<const bf8*>(gb + (long long)p * lddy));
 }
 
-static int ew_blocks(long long n) {
-  long long b = (n + 255) / 256;
-  return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+// pixel blocks per image: enough blocks to cover the chip ~4x, >= 4 pixel passes per block
+static int gn_pix_per_block(int N, int HW, int C8) {
+  const int ppp = C8 >= 256 ? 1 : 256 / C8;
+  int nb = std::max(1, (1024 + N - 1) / N);
+  int ppb = (HW + nb - 1) / nb;
+  ppb = std::max(ppb, 4 * ppp);
+  ppb = (ppb + ppp - 1) / ppp * ppp;
+  return ppb;
 }
 
-// ws: double[4*N*C] scratch.  stats out (fp32): mean[N*G], rstd[N*G], a[N*C], b[N*C]
+// scratch floats otamd_groupnorm_fwd / _bwd need (ws): partial slabs + coefficients + double sums
+OTAMD_API long long otamd_groupnorm_ws_floats(int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % 8) return -1;
+  const int ppb = gn_pix_per_block(N, HW, C / 8);
+  const long long nblk = (HW + ppb - 1) / ppb;
+  return (long long)N * nblk * 2 * C + 3LL * N * C + 4LL * N * C + 64;
+}
+
+// ws: otamd_groupnorm_ws_floats floats.  stats out (fp32): mean[N*G], rstd[N*G], a[N*C], b[N*C]
 OTAMD_API int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long long ldy, int N, int HW, int C, int G,
                                   float eps, const void* gamma, const void* beta, int silu, float* mean, float* rstd,
-                                  float* a, float* b, double* ws, hipStream_t stream) {
+                                  float* a, float* b, float* ws, hipStream_t stream) {
   if (!x || !y || !mean || !rstd || !a || !b || !ws || N <= 0 || HW <= 0 || C <= 0 || G <= 0) return OTAMD_EINVAL;
-  if (C % 8 || C % G || ldx % 8 || ldy % 8 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15) || C > 8192) return OTAMD_EINVAL;
-  if (hipMemsetAsync(ws, 0, sizeof(double) * 2 * N * C, stream) != hipSuccess) return OTAMD_ELAUNCH;
-  const int ppb = 128;
+  if (C % 8 || C % G || ldx % 8 || ldy % 8 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15) || C > 8192 ||
+      ((uintptr_t)ws & 7))
+    return OTAMD_EINVAL;
+  const int C8 = C / 8, nt = gn_threads(C8);
+  if (nt > 512) return OTAMD_EINVAL;
+  const int ppb = gn_pix_per_block(N, HW, C8);
   dim3 grid((HW + ppb - 1) / ppb, N);
-  gn_stats_kernel<<<grid, 256, 2 * C * sizeof(float), stream>>>((const bf16_t*)x, ldx, HW, C, ppb, ws, ws + (long long)N * C);
+  const int ppp = nt / C8;
+  gn_stats_kernel<<<grid, nt, ppp * 2 * C * sizeof(float), stream>>>((const bf16_t*)x, ldx, HW, C, ppb, ws);
   OTAMD_CHECK_LAUNCH();
-  gn_finalize_kernel<<<N, 64, 0, stream>>>(ws, ws + (long long)N * C, HW, C, G, eps, (const bf16_t*)gamma,
-                                           (const bf16_t*)beta, mean, rstd, a, b);
+  double* sums = reinterpret_cast<double*>(ws + (long long)N * grid.x * 2 * C + 3LL * N * C + ((3LL * N * C) & 1));
+  gn_colreduce_kernel<<<dim3((2 * C + 63) / 64, N), 1024, 0, stream>>>(ws, grid.x, 2 * C, sums);
   OTAMD_CHECK_LAUNCH();
-  const long long chunks = (long long)N * HW * (C / 8);
-  if (silu) gn_apply_kernel<true><<<ew_blocks(chunks), 256, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, N, HW, C, a, b);
-  else gn_apply_kernel<false><<<ew_blocks(chunks), 256, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, N, HW, C, a, b);
+  gn_finalize_kernel<<<N, 256, 0, stream>>>(sums, HW, C, G, eps, (const bf16_t*)gamma, (const bf16_t*)beta, mean, rstd,
+                                            a, b);
+  OTAMD_CHECK_LAUNCH();
+  if (silu) gn_apply_kernel<true><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, HW, C, ppb, a, b);
+  else gn_apply_kernel<false><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, HW, C, ppb, a, b);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
 
-// ws: double[2*N*C] + float scratch c1,c2 [2*N*G] given separately in fws
+// ws: otamd_groupnorm_ws_floats floats (8-byte aligned)
 OTAMD_API int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx,
                                   long long lddx, int N, int HW, int C, int G, const void* gamma, int silu,
                                   const float* mean, const float* rstd, const float* a, const float* b,
-                                  void* dgamma, void* dbeta, int param_f32, int param_acc, double* ws, float* fws,
+                                  void* dgamma, void* dbeta, int param_f32, int param_acc, float* ws,
                                   int accumulate, hipStream_t stream) {
-  if (!x || !dy || !dx || !mean || !rstd || !a || !b || !ws || !fws || N <= 0 || HW <= 0) return OTAMD_EINVAL;
-  if (C % 8 || C % G || ldx % 8 || lddy % 8 || lddx % 8 || C > 8192) return OTAMD_EINVAL;
+  if (!x || !dy || !dx || !mean || !rstd || !a || !b || !ws || N <= 0 || HW <= 0) return OTAMD_EINVAL;
+  if (C % 8 || C % G || ldx % 8 || lddy % 8 || lddx % 8 || C > 8192 || ((uintptr_t)ws & 7)) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) return OTAMD_EINVAL;
-  if (hipMemsetAsync(ws, 0, sizeof(double) * 2 * N * C, stream) != hipSuccess) return OTAMD_ELAUNCH;
-  const int ppb = 128;
+  const int C8 = C / 8, nt = gn_threads(C8);
+  if (nt > 512) return OTAMD_EINVAL;
+  const int ppb = gn_pix_per_block(N, HW, C8);
   dim3 grid((HW + ppb - 1) / ppb, N);
-  double* s1 = ws;
-  double* s2 = ws + (long long)N * C;
+  const int ppp = nt / C8;
+  float* part = ws;
+  float* coef = ws + (long long)N * grid.x * 2 * C;
+  double* sums = reinterpret_cast<double*>(coef + 3LL * N * C + ((3LL * N * C) & 1));
   if (silu)
-    gn_bwd_reduce_kernel<true><<<grid, 256, 2 * C * sizeof(float), stream>>>(
-        (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, HW, C, G, ppb, a, b, mean, rstd, s1, s2);
+    gn_bwd_reduce_kernel<true><<<grid, nt, ppp * 2 * C * sizeof(float), stream>>>(
+        (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, HW, C, G, ppb, a, b, mean, rstd, part);
   else
-    gn_bwd_reduce_kernel<false><<<grid, 256, 2 * C * sizeof(float), stream>>>(
-        (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, HW, C, G, ppb, a, b, mean, rstd, s1, s2);
+    gn_bwd_reduce_kernel<false><<<grid, nt, ppp * 2 * C * sizeof(float), stream>>>(
+        (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, HW, C, G, ppb, a, b, mean, rstd, part);
   OTAMD_CHECK_LAUNCH();
-  float* c1 = fws;
-  float* c2 = fws + N * G;
-  gn_bwd_finalize_kernel<<<8, 256, 0, stream>>>(s1, s2, N, HW, C, G, (const bf16_t*)gamma, c1, c2, dgamma, dbeta,
-                                                param_f32, param_acc);
+  gn_colreduce_kernel<<<dim3((2 * C + 63) / 64, N), 1024, 0, stream>>>(part, grid.x, 2 * C, sums);
   OTAMD_CHECK_LAUNCH();
-  const long long chunks = (long long)N * HW * (C / 8);
+  gn_bwd_finalize_kernel<<<N, 256, 0, stream>>>(sums, N, HW, C, G, (const bf16_t*)gamma, mean, rstd, coef);
+  OTAMD_CHECK_LAUNCH();
+  if (dgamma || dbeta) {
+    gn_param_grad_kernel<<<(C + 255) / 256, 256, 0, stream>>>(sums, N, C, dgamma, dbeta, param_f32, param_acc);
+    OTAMD_CHECK_LAUNCH();
+  }
   if (silu)
-    gn_bwd_apply_kernel<true><<<ew_blocks(chunks), 256, 0, stream>>>(
-        (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, N, HW, C, G, (const bf16_t*)gamma, a, b,
-        mean, rstd, c1, c2, accumulate);
+    gn_bwd_apply_kernel<true><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, (bf16_t*)dx,
+                                                        lddx, N, HW, C, ppb, a, b, coef, accumulate);
   else
-    gn_bwd_apply_kernel<false><<<ew_blocks(chunks), 256, 0, stream>>>(
-        (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, N, HW, C, G, (const bf16_t*)gamma, a, b,
-        mean, rstd, c1, c2, accumulate);
+    gn_bwd_apply_kernel<false><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, (bf16_t*)dx,
+                                                         lddx, N, HW, C, ppb, a, b, coef, accumulate);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
@@ -464,11 +570,219 @@ __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float* __res
   }
 }
 
+// ---- LayerNorm, row-group form.  L = C8 / CPL lanes per row (a power of two <= 64), RPW = 64 / L
+// rows per wave; lane li of a row owns the CPL 16-byte chunks c8 = li + L*k.  Several rows per wave
+// with CPL loads per lane in flight keep enough bytes moving for HBM (one row per wave with
+// 1-2 chunks per lane left LN at 15-30 % of the HBM roofline); reductions are xor-shuffles inside
+// the row group.
+__device__ __forceinline__ float group_sum(float v, int L) {
+  for (int o = L >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int CPL>
+__global__ void __launch_bounds__(256) ln_fwd_rows_kernel(const bf16_t* __restrict__ x, long long ldx,
+                                                          bf16_t* __restrict__ y, long long ldy, int rows, int C,
+                                                          float eps, const bf16_t* __restrict__ gamma,
+                                                          const bf16_t* __restrict__ beta, float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out, int L) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane & (L - 1);
+  const int RPW = 64 / L;
+  const long long row = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / L;
+  const bool ok = row < rows;
+  float f[CPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    if (ok) {
+      unpack8(*reinterpret_cast<const bf8*>(x + row * ldx + (li + L * k) * 8), f[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[k][j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += f[k][j];
+  }
+  const float mean = group_sum(s, L) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float d = f[k][j] - mean; q = fmaf(d, d, q); }
+  const float rstd = rsqrtf(group_sum(q, L) / C + eps);
+  if (!ok) return;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c8 = li + L * k;
+    float gf[8], bf[8], o[8];
+    unpack8(*reinterpret_cast<const bf8*>(gamma + c8 * 8), gf);
+    unpack8(*reinterpret_cast<const bf8*>(beta + c8 * 8), bf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f[k][j] - mean) * rstd * gf[j] + bf[j];
+    *reinterpret_cast<bf8*>(y + row * ldy + c8 * 8) = pack8(o);
+  }
+  if (li == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma.  Grid-stride over row groups; the
+// parameter gradients come from ln_param_part_kernel (per-lane dgamma/dbeta accumulators here cost
+// ~16 VGPRs per chunk and pushed CPL=5 rows to one wave per SIMD).
+template <int CPL>
+__global__ void __launch_bounds__(256) ln_bwd_rows_kernel(const bf16_t* __restrict__ x, long long ldx,
+                                                          const bf16_t* __restrict__ dy, long long lddy,
+                                                          bf16_t* __restrict__ dx, long long lddx, int rows, int C,
+                                                          const bf16_t* __restrict__ gamma,
+                                                          const float* __restrict__ mean_in,
+                                                          const float* __restrict__ rstd_in, int accumulate, int L) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & (L - 1), RPW = 64 / L;
+  const long long row = ((long long)blockIdx.x * 4 + w) * RPW + lane / L;
+  if (row >= rows) return;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  bf8 xr[CPL], dr[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c8 = li + L * k;
+    xr[k] = *reinterpret_cast<const bf8*>(x + row * ldx + c8 * 8);
+    dr[k] = *reinterpret_cast<const bf8*>(dy + row * lddy + c8 * 8);
+  }
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    float xf[8], dv[8], gm[8];
+    unpack8(xr[k], xf);
+    unpack8(dr[k], dv);
+    unpack8(*reinterpret_cast<const bf8*>(gamma + (li + L * k) * 8), gm);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = dv[j] * gm[j];
+      s1 += g;
+      s2 = fmaf(g, (xf[j] - mean) * rstd, s2);
+    }
+  }
+  // partial row groups: rows past the end returned above, so every lane of a live group is live
+  const float m1 = group_sum(s1, L) / C, m2 = group_sum(s2, L) / C;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c8 = li + L * k;
+    float xf[8], dv[8], gm[8], o[8];
+    unpack8(xr[k], xf);
+    unpack8(dr[k], dv);
+    unpack8(*reinterpret_cast<const bf8*>(gamma + c8 * 8), gm);
+    float prev[8];
+    if (accumulate) unpack8(*reinterpret_cast<const bf8*>(dx + row * lddx + c8 * 8), prev);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = rstd * (dv[j] * gm[j] - m1 - (xf[j] - mean) * rstd * m2);
+      if (accumulate) o[j] += prev[j];
+    }
+    *reinterpret_cast<bf8*>(dx + row * lddx + c8 * 8) = pack8(o);
+  }
+}
+
+// dgamma / dbeta partials per row slab: part[slab][0|1][c] = sum_rows dy xhat | dy.  Column-tiled
+// (lane = one 16-byte chunk, 64 chunks per block column, 8 waves stride the slab's rows) so every
+// load is a coalesced row segment.  grid (ceil(C8 / 64), slabs), block 512
+__global__ void __launch_bounds__(512) ln_param_part_kernel(const bf16_t* __restrict__ x, long long ldx,
+                                                            const bf16_t* __restrict__ dy, long long lddy, int rows,
+                                                            int C, const float* __restrict__ mean_in,
+                                                            const float* __restrict__ rstd_in, int rps,
+                                                            float* __restrict__ part) {
+  __shared__ float red[8][2][8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int C8 = C >> 3;
+  const int c8 = blockIdx.x * 64 + lane;
+  const bool ok = c8 < C8;
+  const long long r0 = (long long)blockIdx.y * rps;
+  const long long r1 = min((long long)rows, r0 + rps);
+  float dg[8], db[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { dg[j] = 0.f; db[j] = 0.f; }
+  if (ok) {
+#pragma unroll 4
+    for (long long r = r0 + w; r < r1; r += 8) {
+      float xf[8], dv[8];
+      unpack8(*reinterpret_cast<const bf8*>(x + r * ldx + c8 * 8), xf);
+      unpack8(*reinterpret_cast<const bf8*>(dy + r * lddy + c8 * 8), dv);
+      const float m = mean_in[r], rs = rstd_in[r];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dg[j] = fmaf(dv[j], (xf[j] - m) * rs, dg[j]);
+        db[j] += dv[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[w][0][j][lane] = dg[j]; red[w][1][j][lane] = db[j]; }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * 8 * 64; i += 512) {
+    const int wh = i >> 9, j = (i >> 6) & 7, l = i & 63;
+    const int cc8 = blockIdx.x * 64 + l;
+    if (cc8 >= C8) continue;
+    float t = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) t += red[ww][wh][j][l];
+    part[(long long)blockIdx.y * 2 * C + wh * C + cc8 * 8 + j] = t;
+  }
+}
+
+// chunks per lane for a row of C8 16-byte chunks: L = C8 / CPL a power of two <= 64 (0: no fit)
+static int ln_pick(int C8, int* L) {
+  const int cands[] = {5, 4, 3, 6, 2, 8, 1};
+  for (int c : cands) {
+    if (C8 % c) continue;
+    const int l = C8 / c;
+    if (l <= 64 && (l & (l - 1)) == 0) { *L = l; return c; }
+  }
+  return 0;
+}
+
+// sum block partials [nb][2][C] -> dgamma, dbeta: 64 columns x 16 partial lanes per block
+__global__ void __launch_bounds__(1024) ln_param_reduce2_kernel(const float* __restrict__ part, int nb, int C,
+                                                                void* __restrict__ dgamma, void* __restrict__ dbeta,
+                                                                int pf32, int pacc) {
+  __shared__ float red[16][65];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < 2 * C)
+    for (int b = pl; b < nb; b += 16) s += part[(long long)b * 2 * C + c];
+  red[pl][cl] = s;
+  __syncthreads();
+  if (pl == 0 && c < 2 * C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    if (c < C) store_param_grad(dgamma, c, t, pf32, pacc); else store_param_grad(dbeta, c - C, t, pf32, pacc);
+  }
+}
+
 OTAMD_API int otamd_layernorm_fwd(const void* x, long long ldx, void* y, long long ldy, int rows, int C, float eps,
                                   const void* gamma, const void* beta, float* mean, float* rstd, hipStream_t stream) {
   if (!x || !y || !gamma || !beta || !mean || !rstd || rows < 0 || C % 8 || C > 64 * 8 * LN_MAXCH) return OTAMD_EINVAL;
   if (ldx % 8 || ldy % 8 || (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15)) return OTAMD_EINVAL;
   if (rows == 0) return OTAMD_OK;
+  int L = 0;
+  const int cpl = ln_pick(C / 8, &L);
+  if (cpl) {
+    const int rpb = 4 * (64 / L);
+    const int nb = (rows + rpb - 1) / rpb;
+#define LNF(K) ln_fwd_rows_kernel<K><<<nb, 256, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, rows, C, eps, \
+                                                            (const bf16_t*)gamma, (const bf16_t*)beta, mean, rstd, L)
+    switch (cpl) {
+      case 1: LNF(1); break;
+      case 2: LNF(2); break;
+      case 3: LNF(3); break;
+      case 4: LNF(4); break;
+      case 5: LNF(5); break;
+      case 6: LNF(6); break;
+      default: LNF(8); break;
+    }
+#undef LNF
+    OTAMD_CHECK_LAUNCH();
+    return OTAMD_OK;
+  }
   ln_fwd_kernel<<<(rows + 3) / 4, 256, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, rows, C, eps,
                                                     (const bf16_t*)gamma, (const bf16_t*)beta, mean, rstd);
   OTAMD_CHECK_LAUNCH();
@@ -484,6 +798,40 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
   if (!x || !dy || !dx || !gamma || !mean || !rstd || (!dgamma != !dbeta) || !part) return OTAMD_EINVAL;
   if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8 || lddx % 8) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)gamma) & 15) return OTAMD_EINVAL;
+  int L = 0;
+  const int cpl = ln_pick(C / 8, &L);
+  if (cpl) {
+    const int rpb = 4 * (64 / L);
+    const int nbr = (rows + rpb - 1) / rpb;
+#define LNB(K) ln_bwd_rows_kernel<K><<<nbr, 256, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, \
+                                                              (bf16_t*)dx, lddx, rows, C, (const bf16_t*)gamma, mean, \
+                                                              rstd, accumulate, L)
+    switch (cpl) {
+      case 1: LNB(1); break;
+      case 2: LNB(2); break;
+      case 3: LNB(3); break;
+      case 4: LNB(4); break;
+      case 5: LNB(5); break;
+      case 6: LNB(6); break;
+      default: LNB(8); break;
+    }
+#undef LNB
+    OTAMD_CHECK_LAUNCH();
+    if (!dgamma) return OTAMD_OK;
+    // row slabs of >= 64 rows, at most 512 (the part buffer holds 1024 x 2C floats)
+    const int cb = (C / 8 + 63) / 64;
+    int slabs = (rows + 63) / 64;
+    if (slabs > 512) slabs = 512;
+    if (slabs * cb < 1024 && slabs < (rows + 15) / 16) slabs = min((rows + 15) / 16, min(512, 1024 / cb));
+    const int rps = (rows + slabs - 1) / slabs;
+    slabs = (rows + rps - 1) / rps;
+    ln_param_part_kernel<<<dim3(cb, slabs), 512, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, rows, C,
+                                                              mean, rstd, rps, part);
+    OTAMD_CHECK_LAUNCH();
+    ln_param_reduce2_kernel<<<(2 * C + 63) / 64, 1024, 0, stream>>>(part, slabs, C, dgamma, dbeta, param_f32, param_acc);
+    OTAMD_CHECK_LAUNCH();
+    return OTAMD_OK;
+  }
   int nb = (rows + 3) / 4;
   if (nb > 512) nb = 512;
   ln_bwd_kernel<<<nb, 256, 8 * C * sizeof(float), stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy,

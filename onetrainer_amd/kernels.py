@@ -347,7 +347,7 @@ def groupnorm_fwd(x, gamma, beta, groups, eps, silu, out=None):
     rstd = torch.empty(N * groups, dtype=F32, device=dev)
     a = torch.empty(N * C_, dtype=F32, device=dev)
     b = torch.empty(N * C_, dtype=F32, device=dev)
-    ws = workspace(16 * N * C_, dev)
+    ws = workspace(4 * lib().otamd_groupnorm_ws_floats(N, HW, C_), dev)
     check(lib().otamd_groupnorm_fwd(_p(x), ldx, _p(out), ldy, N, HW, C_, groups, float(eps), _p(gamma), _p(beta),
                                     int(silu), _p(mean), _p(rstd), _p(a), _p(b), _p(ws), stream_handle()),
           "otamd_groupnorm_fwd")
@@ -370,11 +370,10 @@ def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, 
         dgamma = torch.empty(C_, dtype=F32, device=dev)
         dbeta = torch.empty(C_, dtype=F32, device=dev)
     pf32 = int(dgamma is not None and dgamma.dtype == F32)
-    ws = workspace(16 * N * C_ + 8 * N * groups + 64, dev)
-    fws = ws[16 * N * C_:].view(torch.float32)
+    ws = workspace(4 * lib().otamd_groupnorm_ws_floats(N, HW, C_), dev)
     check(lib().otamd_groupnorm_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, N, HW, C_, groups, _p(gamma), int(silu),
                                     _p(mean), _p(rstd), _p(a), _p(b), _p(dgamma), _p(dbeta), pf32, int(param_acc),
-                                    _p(ws), _p(fws), int(accumulate), stream_handle()), "otamd_groupnorm_bwd")
+                                    _p(ws), int(accumulate), stream_handle()), "otamd_groupnorm_bwd")
     return dx, dgamma, dbeta
 
 

@@ -1,0 +1,54 @@
+"""Per-step timeline statistics from a rocprofv3 kernel-trace DB: for the last train step (between
+the last two fused-AdamW launches) the busy time of each stream, the union of busy time (GPU
+occupied by >= 1 kernel), the idle gaps, and the per-stream top kernels.
+
+usage: python tools/timeline.py gpurun_out/prof/run_results.db [--marker adamw_bf16_kernel]
+"""
+import argparse
+import collections
+import sqlite3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--marker", default="adamw_bf16_kernel")
+    ap.add_argument("--top", type=int, default=12)
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    rows = c.execute("select name, stream_id, queue_id, start, end from kernels order by start").fetchall()
+    marks = [r[3] for r in rows if a.marker in r[0]]
+    t0, t1 = marks[-3], marks[-2]
+    step = [r for r in rows if t0 < r[3] <= t1]
+    span = (t1 - t0) / 1e6
+    print(f"step span {span:.2f} ms, {len(step)} kernels")
+    by_stream = collections.defaultdict(list)
+    for r in step:
+        by_stream[(r[1], r[2])].append(r)
+    for k, v in by_stream.items():
+        busy = sum(r[4] - r[3] for r in v) / 1e6
+        print(f"  stream {k}: {len(v)} kernels, busy {busy:.2f} ms")
+    iv = sorted((r[3], r[4]) for r in step)
+    union, cs, ce = 0, iv[0][0], iv[0][1]
+    gaps = []
+    for s, e in iv[1:]:
+        if s > ce:
+            union += ce - cs
+            gaps.append(s - ce)
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    union += ce - cs
+    print(f"  union busy {union / 1e6:.2f} ms; idle {span - union / 1e6:.2f} ms in {len(gaps)} gaps "
+          f"(>10us: {sum(1 for g in gaps if g > 10000)}, total {sum(g for g in gaps if g > 10000) / 1e6:.2f} ms)")
+    for k, v in by_stream.items():
+        agg = collections.Counter()
+        for r in v:
+            agg[r[0][:90]] += r[4] - r[3]
+        print(f"  stream {k} top:")
+        for n, d in agg.most_common(a.top):
+            print(f"    {d / 1e6:7.3f} ms  {n}")
+
+
+if __name__ == "__main__":
+    main()
