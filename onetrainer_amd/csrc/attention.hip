@@ -22,6 +22,9 @@
 // on the partial last tile, and the forward's O rescale skipped when no lane's max grew.
 #include "common.h"
 
+#include <mutex>
+#include <unordered_set>
+
 struct AttnArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; bf16_t* o; float* lse;
   const bf16_t* dout; const float* delta; bf16_t* dq; bf16_t* dk; bf16_t* dv; float* dk32; float* dv32;
@@ -607,7 +610,13 @@ static bool attn_ok(const AttnArgs& a) {
 
 template <typename K>
 static void launch(K kern, dim3 grid, int lds, hipStream_t s, const AttnArgs& a) {
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  {   // LDS opt-in once per kernel instance (its LDS size is fixed by the template)
+    static std::mutex mu;
+    static std::unordered_set<const void*> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.insert((const void*)kern).second)
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  }
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
 }
 

@@ -276,26 +276,75 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs args) {
 }
 
 // split-K reduction + the same epilogue: C = alpha * sum_s slab[s] (+bias, +rowvec, +residual) (+C if accumulate)
+// Sum the split-K fp32 slabs and apply the epilogue.  V consecutive columns per thread (8 when
+// N % 8 == 0: one 16-byte bf16 store), every split's loads issued before the adds (the slabs were
+// just written and mostly sit in the MALL: latency, not bandwidth, bounds a dependent chain).
+template <int V>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs args, int splits) {
-  const long long total4 = (long long)args.M * args.N / 4;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total4; i += (long long)gridDim.x * blockDim.x) {
-    const long long e = i * 4;
-    const int m = (int)(e / args.N), n = (int)(e - (long long)m * args.N);
-    float4 s = *reinterpret_cast<const float4*>(args.slab + e);
-    for (int z = 1; z < splits; ++z) {
-      const float4 t = *reinterpret_cast<const float4*>(args.slab + (long long)z * args.M * args.N + e);
-      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  const unsigned NV = (unsigned)args.N / V;
+  const unsigned total = (unsigned)args.M * NV;
+  const long long MN = (long long)args.M * args.N;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const unsigned m = i / NV, n = (i - m * NV) * V;
+    const long long e = (long long)m * args.N + n;
+    float v[V];
+    {
+      const float4 t = *reinterpret_cast<const float4*>(args.slab + e);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+      if constexpr (V == 8) {
+        const float4 u = *reinterpret_cast<const float4*>(args.slab + e + 4);
+        v[4] = u.x; v[5] = u.y; v[6] = u.z; v[7] = u.w;
+      }
     }
-    float v[4] = {s.x * args.alpha, s.y * args.alpha, s.z * args.alpha, s.w * args.alpha};
-    if (args.bias) for (int t = 0; t < 4; ++t) v[t] += bf2f(args.bias[n + t]);
-    if (args.rowvec) for (int t = 0; t < 4; ++t) v[t] += bf2f(args.rowvec[(long long)(m / args.rows_per_vec) * args.ldv + n + t]);
-    if (args.residual) for (int t = 0; t < 4; ++t) v[t] += bf2f(args.residual[(long long)m * args.ldr + n + t]);
+    int z = 1;
+    for (; z + 3 < splits; z += 4) {
+      float4 t[4][V / 4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int h = 0; h < V / 4; ++h) t[q][h] = *reinterpret_cast<const float4*>(args.slab + (z + q) * MN + e + 4 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int h = 0; h < V / 4; ++h) {
+          v[4 * h] += t[q][h].x; v[4 * h + 1] += t[q][h].y; v[4 * h + 2] += t[q][h].z; v[4 * h + 3] += t[q][h].w;
+        }
+    }
+    for (; z < splits; ++z)
+#pragma unroll
+      for (int h = 0; h < V / 4; ++h) {
+        const float4 t = *reinterpret_cast<const float4*>(args.slab + z * MN + e + 4 * h);
+        v[4 * h] += t.x; v[4 * h + 1] += t.y; v[4 * h + 2] += t.z; v[4 * h + 3] += t.w;
+      }
+#pragma unroll
+    for (int t = 0; t < V; ++t) v[t] *= args.alpha;
+    if (args.bias)
+#pragma unroll
+      for (int t = 0; t < V; ++t) v[t] += bf2f(args.bias[n + t]);
+    if (args.rowvec)
+#pragma unroll
+      for (int t = 0; t < V; ++t) v[t] += bf2f(args.rowvec[(long long)(m / args.rows_per_vec) * args.ldv + n + t]);
+    if (args.residual)
+#pragma unroll
+      for (int t = 0; t < V; ++t) v[t] += bf2f(args.residual[(long long)m * args.ldr + n + t]);
     if (args.c_f32) {
       float* dst = reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n;
-      for (int t = 0; t < 4; ++t) dst[t] = args.accumulate ? dst[t] + v[t] : v[t];
+#pragma unroll
+      for (int t = 0; t < V; ++t) dst[t] = args.accumulate ? dst[t] + v[t] : v[t];
     } else {
       bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
-      for (int t = 0; t < 4; ++t) dst[t] = f2bf(args.accumulate ? bf2f(dst[t]) + v[t] : v[t]);
+      if constexpr (V == 8) {
+        if (args.accumulate) {
+          float p[8];
+          unpack8(*reinterpret_cast<const bf8*>(dst), p);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) v[t] += p[t];
+        }
+        *reinterpret_cast<bf8*>(dst) = pack8(v);
+      } else {
+#pragma unroll
+        for (int t = 0; t < V; ++t) dst[t] = f2bf(args.accumulate ? bf2f(dst[t]) + v[t] : v[t]);
+      }
     }
   }
 }
@@ -471,9 +520,13 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
     OTAMD_CHECK_LAUNCH();
   }
   if (splits > 1) {
-    long long t4 = (long long)a.M * a.N / 4;
-    int blocks = (int)std::min<long long>((t4 + 255) / 256, 4096);
-    splitk_reduce_kernel<<<blocks, 256, 0, stream>>>(a, splits);
+    // 8-wide needs 16-byte aligned rows of C (bf16: ldc % 8, fp32 handled element-wise)
+    const bool v8 = (a.N % 8) == 0 && (a.ldc % 8) == 0 && ((uintptr_t)a.C & 15) == 0;
+    const long long nv = (long long)a.M * a.N / (v8 ? 8 : 4);
+    if ((long long)a.M * a.N >= (1LL << 32)) return OTAMD_EINVAL;
+    const int blocks = (int)std::min<long long>((nv + 255) / 256, 8192);
+    if (v8) splitk_reduce_kernel<8><<<blocks, 256, 0, stream>>>(a, splits);
+    else splitk_reduce_kernel<4><<<blocks, 256, 0, stream>>>(a, splits);
     OTAMD_CHECK_LAUNCH();
   }
   return OTAMD_OK;

@@ -13,6 +13,9 @@
 //     flight across the barrier while the current one is multiplied.
 #include "gemm.h"
 
+#include <mutex>
+#include <unordered_set>
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) short4v lds_s4_t;
 #define OFF_INVALID 0x80000000u
@@ -422,9 +425,13 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
   const int lds = 2 * (BMv + BNv) * 128;
-  static bool attr_set[3] = {false, false, false};
-  (void)attr_set;
-  hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  {   // the LDS opt-in once per kernel instance (a per-launch driver call costs host time on every GEMM)
+    static std::mutex mu;
+    static std::unordered_set<const void*> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.insert((const void*)fn).second)
+      hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 256) * 128);
+  }
   hipLaunchKernelGGL(fn, dim3(tiles, a.batch > 1 ? a.batch : 1, splits), dim3(NWv * 64), lds, stream, a, (unsigned)ab,
                      (unsigned)bb, a2b, b2b);
   OTAMD_CHECK_LAUNCH();

@@ -51,8 +51,13 @@ def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     return ws
 
 
+_gemm_forced_splits = 0   # tools/gemm_splits.py probe: forces the split count of planned GEMMs
+
+
 def _gemm(a: GemmArgs, splits: int, device) -> None:
     """splits = 0: the library plans tile shape and split-K (otamd_gemm_plan)."""
+    if splits == 0 and _gemm_forced_splits:
+        splits = _gemm_forced_splits
     s_out = C.c_int(0)
     ws_bytes = lib().otamd_gemm_plan(C.byref(a), splits, C.byref(s_out))
     _req(ws_bytes >= 0, "gemm plan")
