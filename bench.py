@@ -123,6 +123,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true", help="skip the VAE-encode (latent caching) side measurement")
     ap.add_argument("--cpu-res", type=int, default=512)
+    ap.add_argument("--autotune", action="store_true",
+                    help="time (tile, split-K) candidates per GEMM signature in warm-up instead of the analytic plan "
+                         "(measured: no gain on the SDXL step -- isolated warm-cache timings do not transfer)")
     args = ap.parse_args()
 
     from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_sdxl_batch
@@ -149,6 +152,8 @@ def main():
     cfg.learning_rate_warmup_steps = 0
     cfg.resolution = str(args.res)
 
+    from onetrainer_amd import kernels as K
+    K.set_gemm_autotune(args.autotune)   # plans are tuned inside the untimed warm-up steps
     tr = GenericTrainer(cfg)
     t0 = time.time()
     tr.start()
@@ -259,6 +264,8 @@ def main():
                      "step_basis": basis + " x per-GPU images / step time"},
         "cpu_baseline": None,
         "vae_encode": vae,
+        "gemm_plans": "autotuned in warm-up (%d signatures)" % len(K.gemm_autotune_cache()) if args.autotune
+        else "analytic",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not flux:
         del tr

@@ -92,6 +92,12 @@ int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_byt
 /* plan query: workspace bytes otamd_gemm needs for `splits` (0 = automatic tile + split-K plan) */
 long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out);
 
+/* replaces: (plan override) the same GEMM with an explicit plan -- the autotuner's candidates and its
+   cached per-shape choice (kernels.py set_gemm_autotune).  tile: -1 v1 128x128, 0 256x256, 1 256x128,
+   2 128x256, 3 256x256/4 waves; splits >= 1; workspace >= splits*M*N*4 bytes when splits > 1 */
+int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
+                        hipStream_t stream);
+
 /* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves */
 int otamd_gemm_plan_tile(const GemmArgs* in, int splits);
 

@@ -466,7 +466,9 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
   return tile;
 }
 
-OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_bytes, hipStream_t stream) {
+// force_tile: -9 = planned; otherwise the tile code (-1 v1, 0..3 v2) and splits >= 1 as given
+static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* workspace, long long ws_bytes,
+                     hipStream_t stream) {
   if (!in) return OTAMD_EINVAL;
   GemmArgs a = *in;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
@@ -508,7 +510,8 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
   } else {
     a.slab = nullptr;
   }
-  const int tile = resolve_tile(a, splits, plan, v2_only);
+  int tile = force_tile == -9 ? resolve_tile(a, splits, plan, v2_only) : force_tile;
+  if (v2_only && tile < 0) return OTAMD_EUNSUPPORTED;
   int rc = OTAMD_EUNSUPPORTED;
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
@@ -530,6 +533,18 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
     OTAMD_CHECK_LAUNCH();
   }
   return OTAMD_OK;
+}
+
+OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_bytes, hipStream_t stream) {
+  return gemm_impl(in, splits, -9, workspace, ws_bytes, stream);
+}
+
+// explicit plan (the autotuner's candidates and its cached choice): tile -1 = v1 128x128, 0 = 256x256,
+// 1 = 256x128, 2 = 128x256, 3 = 256x256 (4 waves); splits >= 1 (rounded to whole 64-deep K steps)
+OTAMD_API int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
+                                  hipStream_t stream) {
+  if (tile < -1 || tile > 3 || splits < 1) return OTAMD_EINVAL;
+  return gemm_impl(in, splits, tile, workspace, ws_bytes, stream);
 }
 
 OTAMD_API int otamd_gemm_args_size(void) { return (int)sizeof(GemmArgs); }

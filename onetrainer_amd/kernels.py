@@ -53,11 +53,85 @@ def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 
 _gemm_forced_splits = 0   # tools/gemm_splits.py probe: forces the split count of planned GEMMs
 
+# ---- GEMM plan autotuner --------------------------------------------------------------------
+# The library's analytic plan (tile x split-K, gemm.hip plan_gemm) misjudges wave quantisation and
+# the split-K slab traffic on some medium shapes by 10-40 %.  With autotuning on, the first GEMM of
+# each signature times every (tile, splits) candidate on the device (into a scratch output, so
+# accumulating / in-place epilogues are not disturbed) and caches the fastest; later launches use
+# otamd_gemm_explicit.  Candidate plans all compute the same product; they differ only in the fp32
+# summation order of split-K.
+_TUNE = {"on": False, "cache": {}, "reps": 3}
+_TILES = (0, 1, 2, 3, -1)
+_SPLITS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 16)
+
+
+def set_gemm_autotune(on: bool = True) -> None:
+    _TUNE["on"] = bool(on)
+
+
+def gemm_autotune_cache() -> dict:
+    return _TUNE["cache"]
+
+
+def _tune_key(a: GemmArgs) -> tuple:
+    return (a.amode, a.bmode, a.M, a.N, a.K, a.K1 if a.A2 else 0, a.batch, a.c_f32, bool(a.bias), bool(a.rowvec),
+            bool(a.residual), bool(a.accumulate), a.ga.KH, a.ga.stride, a.ga.upsample, a.gb.KH)
+
+
+def _tune(a: GemmArgs, device) -> tuple:
+    v2_only = a.bmode == OPM_CONV_WT or bool(a.A2)   # conv-weight B / second K segment: v2 kernels only
+    torch.cuda.synchronize(device)
+    b = GemmArgs.from_buffer_copy(a)
+    esz = 4 if a.c_f32 else 2
+    rows = a.M * max(1, a.batch)
+    scratch = torch.empty(((rows - 1) * max(a.ldc, a.N) + a.N) * esz + 256, dtype=torch.uint8, device=device)
+    if a.batch > 1:
+        scratch = torch.empty(int(a.sc0 * (a.batch // max(1, a.bdiv)) + a.sc1 * a.bdiv + a.M * a.ldc) * esz + 256,
+                              dtype=torch.uint8, device=device)
+    b.C = _p(scratch)
+    best, best_t, seen = None, float("inf"), set()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for s in (_SPLITS if a.batch <= 1 else (1,)):
+        kps = ((a.K + s - 1) // s + 63) // 64 * 64
+        se = (a.K + kps - 1) // kps
+        if se in seen or (s > 1 and kps < 256):
+            continue
+        seen.add(se)
+        ws_bytes = se * a.M * a.N * 4 if se > 1 else 0
+        ws = workspace(ws_bytes, device) if ws_bytes else None
+        for t in _TILES:
+            if v2_only and t < 0:
+                continue
+            rc = lib().otamd_gemm_explicit(C.byref(b), t, se, _p(ws), ws_bytes, stream_handle())
+            if rc != 0:
+                continue
+            e0.record()
+            for _ in range(_TUNE["reps"]):
+                lib().otamd_gemm_explicit(C.byref(b), t, se, _p(ws), ws_bytes, stream_handle())
+            e1.record()
+            e1.synchronize()
+            dt = e0.elapsed_time(e1)
+            if dt < best_t:
+                best, best_t = (t, se), dt
+    _req(best is not None, "gemm autotune: no candidate plan launched")
+    return best
+
 
 def _gemm(a: GemmArgs, splits: int, device) -> None:
-    """splits = 0: the library plans tile shape and split-K (otamd_gemm_plan)."""
+    """splits = 0: the library plans tile shape and split-K (otamd_gemm_plan), or the autotuner's
+    cached plan when set_gemm_autotune(True)."""
     if splits == 0 and _gemm_forced_splits:
         splits = _gemm_forced_splits
+    if splits == 0 and _TUNE["on"]:
+        key = _tune_key(a)
+        plan = _TUNE["cache"].get(key)
+        if plan is None:
+            plan = _TUNE["cache"][key] = _tune(a, device)
+        t, s = plan
+        ws_bytes = s * a.M * a.N * 4 if s > 1 else 0
+        ws = workspace(ws_bytes, device) if ws_bytes else None
+        check(lib().otamd_gemm_explicit(C.byref(a), t, s, _p(ws), ws_bytes, stream_handle()), "otamd_gemm_explicit")
+        return
     s_out = C.c_int(0)
     ws_bytes = lib().otamd_gemm_plan(C.byref(a), splits, C.byref(s_out))
     _req(ws_bytes >= 0, "gemm plan")

@@ -95,3 +95,42 @@ def test_conv_fwd_dgrad_wgrad(dev, N, H, W, Cin, Cout, stride, up):
     else:
         dx = K.conv2d_dgrad(dy, w, (H, W), stride, 1)
     close(dx, to_nhwc(xr.grad))
+
+
+@pytest.fixture
+def autotune():
+    K.set_gemm_autotune(True)
+    K.gemm_autotune_cache().clear()
+    yield
+    K.set_gemm_autotune(False)
+    K.gemm_autotune_cache().clear()
+
+
+def test_autotuned_plans(dev, autotune):
+    """autotuned (tile, split-K) plans: same products as the fp32 reference, accumulate and in-place
+    residual epilogues untouched by the tuner's candidate runs, cached per signature."""
+    torch.manual_seed(5)
+    x, w = rnd(4096, 1280, dev=dev), rnd(1280, 1280, dev=dev, scale=0.05)
+    r = rnd(4096, 1280, dev=dev)
+    y = K.linear(x, w, residual=r)
+    close(y, x.float() @ w.float().t() + r.float())
+    acc = torch.ones(1280, 1280, device=dev, dtype=torch.float32)
+    dy = rnd(4096, 1280, dev=dev)
+    K.linear_wgrad(dy, x, out=acc, accumulate=True)
+    close(acc, dy.float().t() @ x.float() + 1.0, tol=1e-2)
+    dx = K.linear_dgrad(dy, w)
+    close(dx, dy.float() @ w.float())
+    xc = rnd(2, 32, 32, 320, dev=dev)
+    wc = rnd(320, 3, 3, 320, dev=dev, scale=0.05)
+    yc = K.conv2d(xc, wc, pad=1)
+    ref = F.conv2d(nchw(xc), wc.permute(0, 3, 1, 2).float(), padding=1)
+    close(yc, to_nhwc(ref))
+    dxc = K.conv2d_dgrad(yc, wc, (32, 32), 1, 1)
+    refd = torch.nn.grad.conv2d_input(nchw(xc).shape, wc.permute(0, 3, 1, 2).float(), nchw(yc), padding=1)
+    close(dxc, to_nhwc(refd))
+    n = len(K.gemm_autotune_cache())
+    assert n >= 5
+    for t, s in K.gemm_autotune_cache().values():
+        assert -1 <= t <= 3 and s >= 1
+    K.linear(x, w, residual=r)           # cached: no new entries
+    assert len(K.gemm_autotune_cache()) == n
