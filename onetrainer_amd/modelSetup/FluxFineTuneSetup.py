@@ -6,6 +6,7 @@ import torch
 
 from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
 from ..util.optimizer.adamw_fused import FusedAdamW
+from ..util.optimizer_util import restore_training_state
 from .BaseFluxSetup import BaseFluxSetup
 
 
@@ -37,6 +38,7 @@ class FluxFineTuneSetup(BaseFluxSetup):
                                      weight_decay=oc.weight_decay if oc.weight_decay is not None else 1e-2,
                                      stochastic_rounding=oc.stochastic_rounding)
         model.param_group_mapping = params.unique_name_mapping()
+        restore_training_state(model, config)
 
     def setup_train_device(self, model, config):
         pass

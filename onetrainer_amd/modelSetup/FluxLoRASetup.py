@@ -9,6 +9,7 @@ import torch
 from ..module.lora import LoRAWrapper
 from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
 from ..util.optimizer.adamw_fused import FusedAdamW
+from ..util.optimizer_util import restore_training_state
 from .BaseFluxSetup import BaseFluxSetup
 
 PRESETS = {"attn-mlp": ["attn", "ff.net"], "attn-only": ["attn"], "full": []}
@@ -45,6 +46,9 @@ class FluxLoRASetup(BaseFluxSetup):
             model.transformer_lora = LoRAWrapper(model.transformer, rank=config.lora_rank, alpha=config.lora_alpha,
                                                  module_filter=self.layer_filter(config), prefix="lora_transformer",
                                                  seed=0)
+        if getattr(model, "lora_state_dict", None) is not None:   # LoRA file / backup (LoRALoaderMixin)
+            model.transformer_lora.load_state_dict(model.lora_state_dict)
+            model.lora_state_dict = None
         model.transformer.lora = model.transformer_lora
         params = self.create_parameters(model, config)
         model.parameters = params
@@ -59,6 +63,7 @@ class FluxLoRASetup(BaseFluxSetup):
                                      weight_decay=oc.weight_decay if oc.weight_decay is not None else 1e-2,
                                      stochastic_rounding=oc.stochastic_rounding)
         model.param_group_mapping = params.unique_name_mapping()
+        restore_training_state(model, config)
 
     def setup_train_device(self, model, config):
         pass

@@ -10,6 +10,7 @@ import torch
 from ..module.lora import PRESETS, LoRAUNetWrapper
 from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
 from ..util.optimizer.adamw_fused import FusedAdamW
+from ..util.optimizer_util import restore_training_state
 from .BaseStableDiffusionXLSetup import BaseStableDiffusionXLSetup
 
 
@@ -43,6 +44,9 @@ class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
         if model.unet_lora is None:
             model.unet_lora = LoRAUNetWrapper(model.unet, rank=config.lora_rank, alpha=config.lora_alpha,
                                               module_filter=self.layer_filter(config), seed=0)
+        if getattr(model, "lora_state_dict", None) is not None:   # LoRA file / backup (LoRALoaderMixin)
+            model.unet_lora.load_state_dict(model.lora_state_dict)
+            model.lora_state_dict = None
         model.unet.lora = model.unet_lora
         params = self.create_parameters(model, config)
         model.parameters = params
@@ -57,6 +61,7 @@ class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
                                      weight_decay=oc.weight_decay if oc.weight_decay is not None else 1e-2,
                                      stochastic_rounding=oc.stochastic_rounding)
         model.param_group_mapping = params.unique_name_mapping()
+        restore_training_state(model, config)
 
     def setup_train_device(self, model, config):
         pass

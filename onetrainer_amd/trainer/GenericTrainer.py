@@ -44,6 +44,7 @@ class GenericTrainer:
         self.device = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device(cfg.train_device)
         if self.model is None:
             self.model = create.create_model(cfg, self.device, seed=self.seed)
+        self._load_weights()
         if self.model_setup is None:
             self.model_setup = create.create_model_setup(cfg, self.device, self.rank, self.world)
         self.model_setup.setup_model(self.model, cfg)
@@ -57,6 +58,88 @@ class GenericTrainer:
                                                 cfg.learning_rate_min_factor, cfg.epochs, approx,
                                                 cfg.gradient_accumulation_steps,
                                                 self.model.train_progress.global_step)
+
+    def _load_weights(self):
+        """base / VAE / LoRA weights and a backup to continue from (GenericTrainer.py:92-108 +
+        the model loader); with nothing named the model keeps its seeded random init."""
+        cfg = self.config
+        names = cfg.model_names()
+        if cfg.continue_last_backup:
+            last = cfg.get_last_backup_path()
+            if last:
+                if cfg.training_method == "LORA":
+                    names.lora = last
+                else:
+                    names.base_model = last
+                print(f"Continuing training from backup '{last}'...")
+            else:
+                print("No backup found, continuing without backup...")
+        if names.base_model or names.lora:
+            from ..modelLoader import create_model_loader
+            create_model_loader(cfg.model_type, cfg.training_method).load(self.model, names)
+
+    def backup(self, train_progress: TrainProgress | None = None) -> str | None:
+        """INTERNAL backup to <workspace>/backup/<timestamp>-backup-<global_step>-<epoch>-<epoch_step>
+        (GenericTrainer.py:406-449): model (diffusers layout / LoRA file), optimizer with
+        param_group_mapping, meta.json, onetrainer_config/args.json; rank 0 writes, a failed backup is
+        removed, rolling backups keep the newest `rolling_backup_count`."""
+        import json
+        import os
+        import shutil
+        import traceback
+        from datetime import datetime
+
+        from ..modelSaver import create_model_saver
+        cfg = self.config
+        tp = train_progress or self.model.train_progress
+        if self.world > 1:
+            torch.distributed.barrier()
+        path = None
+        if self.rank == 0:
+            name = f"{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}-backup-{tp.filename_string()}"
+            path = os.path.join(cfg.workspace_dir, "backup", name)
+            try:
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+                create_model_saver(cfg.model_type, cfg.training_method).save(self.model, cfg, "INTERNAL", path)
+                os.makedirs(os.path.join(path, "onetrainer_config"), exist_ok=True)
+                with open(os.path.join(path, "onetrainer_config", "args.json"), "w") as f:
+                    json.dump(cfg.to_settings_dict(), f, indent=4, default=str)
+            except Exception:
+                traceback.print_exc()
+                print("Could not save backup. Check your disk space!")
+                shutil.rmtree(path, ignore_errors=True)
+                path = None
+            finally:
+                if cfg.rolling_backup:
+                    self._prune_backups(cfg.rolling_backup_count)
+        if self.world > 1:
+            torch.distributed.barrier()
+        return path
+
+    def _prune_backups(self, keep: int):
+        import os
+        import shutil
+        root = os.path.join(self.config.workspace_dir, "backup")
+        if os.path.exists(root):
+            dirs = sorted((d for d in os.listdir(root) if os.path.isdir(os.path.join(root, d))), reverse=True)
+            for d in dirs[keep:]:
+                shutil.rmtree(os.path.join(root, d), ignore_errors=True)
+
+    def save(self, destination: str | None = None, output_format: str | None = None, dtype=None) -> str:
+        """final model (GenericTrainer.py:752-790): config.output_model_destination / _format."""
+        from ..modelSaver import create_model_saver
+        cfg = self.config
+        dest = destination or cfg.output_model_destination
+        if self.rank == 0:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            create_model_saver(cfg.model_type, cfg.training_method).save(self.model, cfg,
+                                                                          output_format or cfg.output_model_format,
+                                                                          dest, dtype)
+        if self.world > 1:
+            torch.distributed.barrier()
+        return dest
 
     def _is_update_step(self, tp: TrainProgress) -> bool:
         return (tp.global_step + 1) % self.config.gradient_accumulation_steps == 0

@@ -91,6 +91,16 @@ class TrainConfig:
     text_encoder_2: ModelPartConfig = field(default_factory=lambda: ModelPartConfig(train=False))
     vae: ModelPartConfig = field(default_factory=lambda: ModelPartConfig(train=False))
     prior: ModelPartConfig = field(default_factory=ModelPartConfig)
+    # model names, output, backups (TrainConfig.py base_model_name / output_* / backup fields)
+    base_model_name: str = ""
+    vae_model_name: str = ""
+    lora_model_name: str = ""
+    output_model_destination: str = ""
+    output_model_format: str = "SAFETENSORS"
+    workspace_dir: str = "workspace/run"
+    continue_last_backup: bool = False
+    rolling_backup: bool = False
+    rolling_backup_count: int = 3
     # build-only (not in the reference): data parallel + gradient bucket size
     dp_bucket_mb: int = 256
     extra: dict = field(default_factory=dict)
@@ -118,6 +128,26 @@ class TrainConfig:
     def load(path: str) -> "TrainConfig":
         with open(path) as f:
             return TrainConfig().from_dict(json.load(f))
+
+    def model_names(self):
+        from ..ModelNames import ModelNames
+        return ModelNames(base_model=self.base_model_name, vae_model=self.vae_model_name, lora=self.lora_model_name)
+
+    def get_last_backup_path(self) -> str | None:
+        """newest directory under <workspace>/backup by name (TrainConfig.py:704-717)."""
+        import os
+        root = os.path.join(self.workspace_dir, "backup")
+        if os.path.exists(root):
+            dirs = sorted((d for d in os.listdir(root) if os.path.isdir(os.path.join(root, d))), reverse=True)
+            if dirs:
+                return os.path.join(root, dirs[0])
+        return None
+
+    def to_settings_dict(self) -> dict:
+        from dataclasses import asdict
+        d = asdict(self)
+        d.update(d.pop("extra"))
+        return d
 
     def resolution_hw(self) -> tuple[int, int]:
         r = str(self.resolution)

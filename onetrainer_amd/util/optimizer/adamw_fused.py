@@ -150,9 +150,12 @@ class FusedAdamW(torch.optim.Optimizer):
             gd = {k: v for k, v in g.items() if k != "params"}
             gd["params"] = ids
             groups.append(gd)
-        return {"state": state, "param_groups": groups}
+        # the stochastic-rounding stream position, so that a resumed run rounds like an uninterrupted one
+        return {"state": state, "param_groups": groups, "sr_seed": int(self.seed)}
 
     def load_state_dict(self, sd):
+        if "sr_seed" in sd:
+            self.seed = int(sd["sr_seed"])
         idx = 0
         for gi, (g, gsd) in enumerate(zip(self.param_groups, sd["param_groups"])):
             for k, v in gsd.items():

@@ -1,0 +1,179 @@
+"""Weight loading / saving and backup layout on CPU.
+
+Golden LDM names below are read off the reference's conversion tables
+(modules/util/convert/convert_sdxl_diffusers_to_ckpt.py:8-81, convert_diffusers_to_ckpt_util.py:232-291,
+convert_sd_diffusers_to_ckpt.py); the tensor counts are the SDXL / SD 1.5 UNet parameter counts
+(1 680 tensors for SDXL)."""
+import json
+import os
+
+import pytest
+import torch
+from safetensors.torch import save_file
+
+from onetrainer_amd.modelLoader import ldm_convert as LC
+from onetrainer_amd.modelLoader.HFModelLoaderMixin import read_diffusers_sub_module
+from onetrainer_amd.modelLoader.StableDiffusionModelLoader import StableDiffusionXLModelLoader, load_vae_encoder
+from onetrainer_amd.modelSaver import StableDiffusionXLModelSaver, save_sub_module, schedule_buffers
+from onetrainer_amd.model.StableDiffusionXLModel import NoiseScheduler, StableDiffusionXLModel
+from onetrainer_amd.module import unet as U
+from onetrainer_amd.module import vae as V
+from onetrainer_amd.util.ModelNames import ModelNames
+from onetrainer_amd.util.optimizer_util import remap_optimizer_state_dict
+
+CPU = torch.device("cpu")
+
+SDXL_GOLDEN = {
+    "down_blocks.1.attentions.0.transformer_blocks.1.attn1.to_q.weight":
+        "input_blocks.4.1.transformer_blocks.1.attn1.to_q.weight",
+    "down_blocks.0.downsamplers.0.conv.weight": "input_blocks.3.0.op.weight",
+    "down_blocks.1.downsamplers.0.conv.bias": "input_blocks.6.0.op.bias",
+    "down_blocks.2.resnets.0.conv_shortcut.weight": "input_blocks.7.0.skip_connection.weight",
+    "down_blocks.2.attentions.1.transformer_blocks.9.ff.net.0.proj.weight":
+        "input_blocks.8.1.transformer_blocks.9.ff.net.0.proj.weight",
+    "mid_block.attentions.0.proj_in.weight": "middle_block.1.proj_in.weight",
+    "mid_block.resnets.1.time_emb_proj.bias": "middle_block.2.emb_layers.1.bias",
+    "up_blocks.0.upsamplers.0.conv.weight": "output_blocks.2.2.conv.weight",
+    "up_blocks.1.upsamplers.0.conv.bias": "output_blocks.5.2.conv.bias",
+    "up_blocks.1.attentions.2.norm.weight": "output_blocks.5.1.norm.weight",
+    "up_blocks.2.resnets.2.norm2.weight": "output_blocks.8.0.out_layers.0.weight",
+    "up_blocks.2.resnets.0.conv1.weight": "output_blocks.6.0.in_layers.2.weight",
+    "add_embedding.linear_2.weight": "label_emb.0.2.weight",
+    "time_embedding.linear_1.bias": "time_embed.0.bias",
+    "conv_in.weight": "input_blocks.0.0.weight",
+    "conv_norm_out.bias": "out.0.bias",
+    "conv_out.weight": "out.2.weight",
+}
+SD15_GOLDEN = {
+    "up_blocks.0.upsamplers.0.conv.weight": "output_blocks.2.1.conv.weight",
+    "up_blocks.1.upsamplers.0.conv.weight": "output_blocks.5.2.conv.weight",
+    "down_blocks.3.resnets.1.conv2.weight": "input_blocks.11.0.out_layers.3.weight",
+    "down_blocks.2.downsamplers.0.conv.weight": "input_blocks.9.0.op.weight",
+    "up_blocks.3.attentions.2.proj_out.weight": "output_blocks.11.1.proj_out.weight",
+    "mid_block.resnets.0.norm1.weight": "middle_block.0.in_layers.0.weight",
+}
+VAE_GOLDEN = {
+    "encoder.down_blocks.1.resnets.0.conv_shortcut.weight": "encoder.down.1.block.0.nin_shortcut.weight",
+    "encoder.down_blocks.0.downsamplers.0.conv.weight": "encoder.down.0.downsample.conv.weight",
+    "encoder.mid_block.resnets.1.norm2.bias": "encoder.mid.block_2.norm2.bias",
+    "encoder.mid_block.attentions.0.to_out.0.weight": "encoder.mid.attn_1.proj_out.weight",
+    "encoder.mid_block.attentions.0.group_norm.weight": "encoder.mid.attn_1.norm.weight",
+    "encoder.conv_norm_out.weight": "encoder.norm_out.weight",
+    "quant_conv.bias": "quant_conv.bias",
+}
+
+
+def test_ldm_names_golden_and_bijective():
+    for cfg, golden, count in ((U.sdxl_config(), SDXL_GOLDEN, 1680), (U.sd15_config(), SD15_GOLDEN, 686)):
+        specs = U.unet_specs(cfg)
+        names = {n: LC.unet_ldm_name(n, cfg) for n, *_ in specs}
+        assert len(specs) == count and len(set(names.values())) == count
+        for d, ldm in golden.items():
+            assert names[d] == ldm, (d, names[d], ldm)
+    vspecs = V.vae_encoder_specs(V.sdxl_vae_config())
+    vn = {n: LC.vae_ldm_name(n) for n, *_ in vspecs}
+    assert len(set(vn.values())) == len(vspecs)
+    for d, ldm in VAE_GOLDEN.items():
+        assert vn[d] == ldm
+
+
+def _model(seed):
+    unet = U.UNet2DConditionModel(U.tiny_sdxl_config(), CPU, seed=seed)
+    m = StableDiffusionXLModel(unet, NoiseScheduler(CPU))
+    m.vae_encoder = V.AutoencoderKLEncoder(V.tiny_vae_config(), CPU, seed=seed)
+    return m
+
+
+def _same(a, b):
+    sa, sb = a.state_dict(), b.state_dict()
+    return sa.keys() == sb.keys() and all(torch.equal(sa[k], sb[k]) for k in sa)
+
+
+def test_diffusers_dir_roundtrip(tmp_path):
+    src, dst = _model(0), _model(1)
+    assert not _same(src.unet, dst.unet)
+    StableDiffusionXLModelSaver().save(src, None, "DIFFUSERS", str(tmp_path / "m"))
+    assert os.path.isfile(tmp_path / "m" / "unet" / "diffusion_pytorch_model.safetensors")
+    cfg = json.load(open(tmp_path / "m" / "unet" / "config.json"))
+    assert cfg["block_out_channels"] == list(U.tiny_sdxl_config().block_out_channels)
+    StableDiffusionXLModelLoader().load(dst, ModelNames(base_model=str(tmp_path / "m")))
+    assert _same(src.unet, dst.unet) and _same(src.vae_encoder, dst.vae_encoder)
+
+
+def test_sharded_and_pickle_fallback(tmp_path):
+    src = _model(0)
+    sd = {k: v.contiguous() for k, v in src.unet.state_dict().items()}
+    save_sub_module(sd, str(tmp_path / "sh" / "unet"), max_shard_bytes=200_000)
+    assert os.path.isfile(tmp_path / "sh" / "unet" / "diffusion_pytorch_model.safetensors.index.json")
+    got = read_diffusers_sub_module(str(tmp_path / "sh"), "unet")
+    assert got.keys() == sd.keys() and all(torch.equal(got[k], sd[k]) for k in sd)
+    os.makedirs(tmp_path / "pk" / "unet")
+    torch.save({"state_dict": sd}, tmp_path / "pk" / "unet" / "diffusion_pytorch_model.bin")
+    got = read_diffusers_sub_module(str(tmp_path / "pk"), "unet")
+    assert all(torch.equal(got[k], sd[k]) for k in sd)
+
+
+def test_single_file_ldm_roundtrip(tmp_path):
+    src, dst = _model(0), _model(2)
+    f = str(tmp_path / "model.safetensors")
+    StableDiffusionXLModelSaver().save(src, None, "SAFETENSORS", f)
+    from safetensors.torch import load_file
+    sd = load_file(f)
+    assert "model.diffusion_model.input_blocks.0.0.weight" in sd and "first_stage_model.encoder.conv_in.weight" in sd
+    assert sd["first_stage_model.encoder.mid.attn_1.q.weight"].dim() == 4     # LDM 1x1 conv form
+    ref = schedule_buffers(NoiseScheduler(CPU).betas)
+    assert torch.allclose(sd["alphas_cumprod"], ref["alphas_cumprod"]) and sd["betas"].shape == (1000,)
+    StableDiffusionXLModelLoader().load(dst, ModelNames(base_model=f))
+    assert _same(src.unet, dst.unet) and _same(src.vae_encoder, dst.vae_encoder)
+
+
+def test_legacy_vae_attention_names(tmp_path):
+    src, dst = _model(0), _model(3)
+    sd = src.vae_encoder.state_dict()
+    legacy = {}
+    for k, v in sd.items():
+        for new, old in (("to_q", "query"), ("to_k", "key"), ("to_v", "value"), ("to_out.0", "proj_attn")):
+            k = k.replace(f".attentions.0.{new}.", f".attentions.0.{old}.")
+        legacy[k] = v.contiguous()
+    os.makedirs(tmp_path / "v" / "vae")
+    save_file(legacy, str(tmp_path / "v" / "vae" / "diffusion_pytorch_model.safetensors"))
+    load_vae_encoder(dst.vae_encoder, str(tmp_path / "v"))
+    assert _same(src.vae_encoder, dst.vae_encoder)
+
+
+def test_load_failure_message(tmp_path):
+    with pytest.raises(Exception, match="could not load model"):
+        StableDiffusionXLModelLoader().load(_model(0), ModelNames(base_model=str(tmp_path / "missing")))
+
+
+def test_optimizer_state_remap():
+    """create.py:1040-1086: groups matched by unique name; lr / initial_lr from the new config."""
+    old = {"state": {0: {"step": 3}, 1: {"step": 3}, 2: {"step": 5}},
+           "param_groups": [{"params": [0, 1], "lr": 1.0, "initial_lr": 1.0, "weight_decay": 0.5},
+                            {"params": [2], "lr": 2.0, "initial_lr": 2.0, "weight_decay": 0.1}],
+           "param_group_mapping": ["unet", "te"], "param_group_optimizer_mapping": ["ADAMW", "ADAMW"]}
+    new = {"state": {}, "param_groups": [{"params": [0], "lr": 9.0, "initial_lr": 9.0, "weight_decay": 0.0},
+                                         {"params": [1, 2], "lr": 7.0, "initial_lr": 7.0, "weight_decay": 0.0},
+                                         {"params": [3], "lr": 5.0, "initial_lr": 5.0, "weight_decay": 0.0}]}
+    r = remap_optimizer_state_dict(old, new, ["te", "unet", "fresh"], "ADAMW")
+    g = r["param_groups"]
+    assert g[0]["params"] == [0] and g[0]["lr"] == 9.0 and g[0]["weight_decay"] == 0.1
+    assert g[1]["params"] == [1, 2] and g[1]["lr"] == 7.0 and g[1]["weight_decay"] == 0.5
+    assert g[2]["params"] == [3] and g[2]["lr"] == 5.0
+    assert r["state"] == {0: {"step": 5}, 1: {"step": 3}, 2: {"step": 3}}
+    other = remap_optimizer_state_dict(old, new, ["te", "unet", "fresh"], "PRODIGY")
+    assert other["state"] == {}
+
+
+def test_flux_diffusers_roundtrip(tmp_path):
+    from onetrainer_amd.model.FluxModel import FluxModel
+    from onetrainer_amd.modelLoader.FluxModelLoader import FluxModelLoader
+    from onetrainer_amd.modelSaver import FluxModelSaver
+    from onetrainer_amd.module import flux as FX
+    src = FluxModel(FX.FluxTransformer2DModel(FX.tiny_flux_config(), CPU, seed=0))
+    dst = FluxModel(FX.FluxTransformer2DModel(FX.tiny_flux_config(), CPU, seed=1))
+    FluxModelSaver().save(src, None, "DIFFUSERS", str(tmp_path / "flux"))
+    cfg = json.load(open(tmp_path / "flux" / "transformer" / "config.json"))
+    assert cfg["num_layers"] == 2 and cfg["num_single_layers"] == 2
+    FluxModelLoader().load(dst, ModelNames(base_model=str(tmp_path / "flux")))
+    assert _same(src.transformer, dst.transformer)
