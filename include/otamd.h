@@ -202,6 +202,26 @@ int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, long long 
 /* replaces: diffusers GEGLU (ff.net.0) hidden * gelu(gate) */
 int otamd_geglu_fwd(const void* h, long long ldh, void* out, long long ldo, int M, int F, hipStream_t s);
 
+/* ---- text-encoder caching: CLIP-L / CLIP-bigG / T5 forward ---------------- */
+/* replaces: CLIPTextEmbeddings / T5 embed_tokens (transformers, called from model/util/clip_util.py:26-31,
+   t5_util.py:17-22): out[r] = tok[ids[r]] (+ pos[r % T]); ids clamped to [0, vocab) */
+int otamd_embed_tokens(const long long* ids, long long n, int T, const void* tok, const void* pos, void* out, int D,
+                       int vocab, hipStream_t stream);
+/* replaces: CLIPMLP activation (quick_gelu CLIP-L = 0, erf gelu bigG = 1) / gelu_new (2); y may alias x */
+int otamd_act_fwd(const void* x, long long ldx, void* y, long long ldy, long long rows, int C, int kind,
+                  hipStream_t stream);
+/* replaces: T5DenseGatedActDense's act(wi_0 x) * wi_1 x over the fused [wi_0 | wi_1] projection */
+int otamd_gated_act_fwd(const void* h, long long ldh, void* out, long long ldo, long long rows, int F, int kind,
+                        hipStream_t stream);
+/* replaces: T5LayerNorm (RMS norm, fp32 statistics, no bias) */
+int otamd_rmsnorm_fwd(const void* x, long long ldx, void* y, long long ldy, long long rows, int C, float eps,
+                      const void* w, hipStream_t stream);
+/* replaces: the softmax of CLIPAttention (causal mask) and T5Attention (scores + relative position bias):
+   P[r] = softmax(scale S[r] + bias[q, c, h]) with r = (b H + h) Nq + q; causal masks c > q */
+int otamd_softmax_masked_fwd(const float* S, long long lds, void* P, long long ldp, long long rows, int ncols,
+                             int ncols_pad, float scale, int Nq, int H, int causal, const void* bias, long long bsq,
+                             long long bsc, long long bsh, hipStream_t stream);
+
 /* replaces: autograd of GEGLU */
 int otamd_geglu_bwd(const void* h, long long ldh, const void* dout, long long lddo, void* dh, long long lddh,
     int M, int F, hipStream_t s);

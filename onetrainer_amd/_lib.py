@@ -104,6 +104,11 @@ SIGNATURES: dict[str, list] = {
     "otamd_softmax_rows_bwd": [VP, LL, VP, LL, VP, LL, LL, I, I, F, VP],
     # elementwise.hip
     "otamd_geglu_fwd": [VP, LL, VP, LL, I, I, VP],
+    "otamd_embed_tokens": [VP, LL, I, VP, VP, VP, I, I, VP],
+    "otamd_act_fwd": [VP, LL, VP, LL, LL, I, I, VP],
+    "otamd_gated_act_fwd": [VP, LL, VP, LL, LL, I, I, VP],
+    "otamd_rmsnorm_fwd": [VP, LL, VP, LL, LL, I, F, VP, VP],
+    "otamd_softmax_masked_fwd": [VP, LL, VP, LL, LL, I, I, F, I, I, I, VP, LL, LL, LL, VP],
     "otamd_geglu_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP],
     "otamd_silu_fwd": [VP, VP, LL, VP],
     "otamd_silu_bwd": [VP, VP, VP, LL, VP],

@@ -49,11 +49,15 @@ def scale_crop(img: torch.Tensor, scale_res, crop_res, offset):
 
 
 class LatentCacheWriter:
-    def __init__(self, encode_fn, cache_dir: str, bucketing, device, encode_batch: int = 8, rank: int = 0):
+    def __init__(self, encode_fn, cache_dir: str, bucketing, device, encode_batch: int = 8, rank: int = 0,
+                 text_fn=None):
         """encode_fn: [B, 3, H, W] fp32 [0, 1] on `device` -> latent NHWC fp32 [B, H/8, W/8, 4]
-        (module.vae.AutoencoderKLEncoder.encode)."""
+        (module.vae.AutoencoderKLEncoder.encode).  text_fn (optional): {name: int64 token ids [B, T]}
+        on `device` -> {cache key: [B, ...]} (module.text_encoder.encode_sdxl_text & co.), applied to
+        samples that carry "tokens" -- the reference's text-encoder caching step."""
         self.encode_fn, self.cache_dir, self.bucketing = encode_fn, cache_dir, bucketing
         self.device, self.encode_batch, self.rank = torch.device(device), encode_batch, rank
+        self.text_fn = text_fn
 
     def write(self, samples):
         """samples: iterable of dicts {"image": PIL / tensor, optional "text": {name: tensor}}.
@@ -65,7 +69,7 @@ class LatentCacheWriter:
             h, w = img.shape[1], img.shape[2]
             scale_res, crop_res = self.bucketing.bucket_for(h, w)
             off = crop_offset(scale_res, crop_res)
-            prepared.append((i, img, (h, w), scale_res, crop_res, off, s.get("text") or {}))
+            prepared.append((i, img, (h, w), scale_res, crop_res, off, dict(s.get("text") or {}), s.get("tokens")))
         by_res: dict = {}
         for p in prepared:
             by_res.setdefault(tuple(p[4]), []).append(p)
@@ -76,6 +80,13 @@ class LatentCacheWriter:
                 chunk = group[k:k + self.encode_batch]
                 imgs = torch.stack([scale_crop(p[1], p[3], p[4], p[5]) for p in chunk]).to(self.device)
                 lat = self.encode_fn(imgs).float().cpu()
+                tok = [p for p in chunk if p[7] is not None]
+                if tok and self.text_fn is not None:
+                    names = list(tok[0][7])
+                    states = self.text_fn({n: torch.stack([torch.as_tensor(p[7][n], dtype=torch.int64)
+                                                           for p in tok]).to(self.device) for n in names})
+                    for j, p in enumerate(tok):
+                        p[6].update({k2: v[j].to(torch.bfloat16) for k2, v in states.items()})
                 for p, l_ in zip(chunk, lat):
                     i = p[0]
                     rec = {"latent_image": l_.contiguous(),

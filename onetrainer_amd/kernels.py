@@ -1024,3 +1024,70 @@ def flux_unpack(tok, B, h, w, C_):
     out = torch.empty((B, h, w, C_), dtype=BF16, device=tok.device)
     check(lib().otamd_flux_pack(_p(tok), _p(out), B, h, w, C_, C_, 1, stream_handle()), "otamd_flux_pack")
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# text-encoder caching (csrc/text.hip): CLIP-L / CLIP-bigG / T5 forward
+ACT_QUICK_GELU, ACT_GELU_ERF, ACT_GELU_TANH = 0, 1, 2
+
+
+def embed_tokens(ids: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor | None = None) -> torch.Tensor:
+    """ids int64 [B, T] -> bf16 [B*T, D] = tok[ids] (+ pos[t])."""
+    _req(ids.dtype == torch.int64 and ids.is_contiguous() and ids.dim() == 2, "ids: int64 [B, T]")
+    _req(tok.dtype == BF16 and tok.is_contiguous() and (pos is None or (pos.dtype == BF16 and pos.is_contiguous())),
+         "embedding tables: contiguous bf16")
+    B, T = ids.shape
+    V, D = tok.shape
+    _req(pos is None or (pos.shape[1] == D and pos.shape[0] >= T), "position table shape")
+    out = torch.empty((B * T, D), dtype=BF16, device=tok.device)
+    check(lib().otamd_embed_tokens(_p(ids), B * T, T, _p(tok), _p(pos), _p(out), D, V, stream_handle()),
+          "otamd_embed_tokens")
+    return out
+
+
+def act_fwd(x: torch.Tensor, kind: int, out=None) -> torch.Tensor:
+    _req(x.dtype == BF16 and x.dim() == 2 and x.stride(1) == 1, "act: bf16 [rows, C]")
+    out = x if out is None else out
+    check(lib().otamd_act_fwd(_p(x), x.stride(0), _p(out), out.stride(0), x.shape[0], x.shape[1], kind,
+                              stream_handle()), "otamd_act_fwd")
+    return out
+
+
+def gated_act_fwd(h: torch.Tensor, kind: int) -> torch.Tensor:
+    """h = [a | g] -> act(a) * g."""
+    _req(h.dtype == BF16 and h.dim() == 2 and h.stride(1) == 1 and h.shape[1] % 2 == 0, "gated act: bf16 [rows, 2F]")
+    F_ = h.shape[1] // 2
+    out = torch.empty((h.shape[0], F_), dtype=BF16, device=h.device)
+    check(lib().otamd_gated_act_fwd(_p(h), h.stride(0), _p(out), F_, h.shape[0], F_, kind, stream_handle()),
+          "otamd_gated_act_fwd")
+    return out
+
+
+def rmsnorm_fwd(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    _req(x.dtype == BF16 and x.dim() == 2 and x.stride(1) == 1 and w.dtype == BF16 and w.is_contiguous(), "rmsnorm")
+    out = torch.empty(x.shape, dtype=BF16, device=x.device)
+    check(lib().otamd_rmsnorm_fwd(_p(x), x.stride(0), _p(out), out.stride(0), x.shape[0], x.shape[1], float(eps),
+                                  _p(w), stream_handle()), "otamd_rmsnorm_fwd")
+    return out
+
+
+def attn_masked_fwd(q, k, v, heads, scale=1.0, causal=False, bias=None, bias_strides=(0, 0, 0), out=None):
+    """forward-only materialized attention with CLIP's causal mask and/or T5's additive position bias
+    (bf16 bias[q * bsq + c * bsc + h * bsh]): S = q k^T (fp32) -> masked softmax -> o = P v."""
+    B, Nq, Nk, Nkp, D = _mat_geom(q, k, heads)
+    H = heads
+    kp, vp = _pad_keys(k, Nkp), _pad_keys(v, Nkp)
+    S = torch.empty((B * H, Nq, Nkp), dtype=F32, device=q.device)
+    gemm_batched(q, q.stride(1), OPM_K, kp, kp.stride(1), OPM_K, S, Nkp, Nq, Nkp, D, B * H, H,
+                 (q.stride(0), D), (kp.stride(0), D), (H * Nq * Nkp, Nq * Nkp))
+    P = torch.empty((B * H, Nq, Nkp), dtype=BF16, device=q.device)
+    _req(bias is None or (bias.dtype == BF16 and bias.is_contiguous()), "bias: contiguous bf16")
+    check(lib().otamd_softmax_masked_fwd(_p(S), Nkp, _p(P), Nkp, B * H * Nq, Nk, Nkp, float(scale), Nq, H,
+                                         int(causal), _p(bias), *bias_strides, stream_handle()),
+          "otamd_softmax_masked_fwd")
+    del S
+    if out is None:
+        out = torch.empty(q.shape, dtype=BF16, device=q.device)
+    gemm_batched(P, Nkp, OPM_K, vp, vp.stride(1), OPM_MN, out, out.stride(1), Nq, D, Nkp, B * H, H,
+                 (H * Nq * Nkp, Nq * Nkp), (vp.stride(0), D), (out.stride(0), D))
+    return out

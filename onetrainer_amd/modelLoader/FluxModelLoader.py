@@ -8,7 +8,7 @@ import os
 import traceback
 
 from .HFModelLoaderMixin import read_diffusers_sub_module, read_single_file
-from .StableDiffusionModelLoader import load_internal_data
+from .StableDiffusionModelLoader import load_internal_data, load_text_encoders
 
 
 def apply_flux_state_dict(transformer, sd: dict) -> None:
@@ -32,6 +32,7 @@ class FluxModelLoader:
             stacktraces.append(traceback.format_exc())
         try:
             apply_flux_state_dict(model.transformer, read_diffusers_sub_module(base, "transformer"))
+            load_text_encoders(model, base)
             return
         except Exception:
             stacktraces.append(traceback.format_exc())

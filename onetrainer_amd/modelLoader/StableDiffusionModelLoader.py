@@ -5,8 +5,10 @@ Load order and failure behaviour of modules/modelLoader/stableDiffusionXL/Stable
 layout + optimizer / train progress, InternalModelLoaderMixin.py:16-42) -> diffusers directory
 (`unet/`, `vae/` sub-modules, HFModelLoaderMixin.py) -> single-file .safetensors -> single-file
 .ckpt (LDM layout, converted with ldm_convert.py); each failure's traceback is printed and the last
-resort raises Exception("could not load model: <name>").  Text encoders and tokenizers are not
-loaded: the train step consumes cached text states.
+resort raises Exception("could not load model: <name>").  Text encoders (`text_encoder/`,
+`text_encoder_2/`) are loaded into the caching encoders a model carries as text_encoder_1/2
+(module/text_encoder.py); the train step itself consumes cached text states.
+Tokenizers are host-side text processing and stay with the caller.
 
 LoRA (modules/modelLoader/mixin/LoRALoaderMixin.py): `lora` names either an INTERNAL backup directory
 (`lora/lora.safetensors` + internal data) or a .safetensors file in the reference's
@@ -23,7 +25,7 @@ import torch
 
 from ..util.TrainProgress import TrainProgress
 from . import ldm_convert as LC
-from .HFModelLoaderMixin import read_diffusers_sub_module, read_single_file
+from .HFModelLoaderMixin import TRANSFORMERS_FILES, read_diffusers_sub_module, read_single_file, read_sub_module_state_dict
 
 
 def load_internal_data(model, path: str) -> None:
@@ -72,11 +74,34 @@ def load_vae_encoder(encoder, name: str) -> None:
     apply_vae_state_dict(encoder, LC.vae_from_ldm(read_single_file(name), encoder.specs))
 
 
+def load_text_encoder(encoder, root: str, subfolder: str) -> None:
+    """a transformers text encoder (`text_encoder/`, `text_encoder_2/`: model.safetensors, sharded
+    index or pytorch_model.bin) into a module.text_encoder encoder; CLIP keys without the
+    `text_model.` prefix (CLIPTextModel saved by transformers 5.x) are normalised."""
+    sd = read_sub_module_state_dict(root, subfolder, *TRANSFORMERS_FILES)
+    names = {n for n, _ in encoder.specs}
+    fixed = {}
+    for k, v in sd.items():
+        if k not in names and "text_model." + k in names:
+            k = "text_model." + k
+        fixed[k] = v
+    encoder.load_state_dict(fixed)
+
+
+def load_text_encoders(model, root: str, subfolders=("text_encoder", "text_encoder_2")) -> None:
+    """the model's attached caching text encoders (attributes text_encoder_1 / text_encoder_2), if any."""
+    for attr, sub in zip(("text_encoder_1", "text_encoder_2"), subfolders):
+        enc = getattr(model, attr, None)
+        if enc is not None:
+            load_text_encoder(enc, root, sub)
+
+
 class StableDiffusionXLModelLoader:
     """also serves SD 1.5 (the UNet config on the model decides the key layout)."""
 
     def _load_diffusers(self, model, base: str, vae: str | None):
         apply_unet_state_dict(model.unet, read_diffusers_sub_module(base, "unet"))
+        load_text_encoders(model, base)
         enc = getattr(model, "vae_encoder", None)
         if enc is not None:
             load_vae_encoder(enc, vae or base)
