@@ -126,7 +126,22 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16_t* __res
   const int r1 = min(min(M, (g + 1) * rows_per_group), r0 + rpb);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (col < N) {
-    for (int m = r0 + rl; m < r1; m += 8) {
+    // 8 independent 16-byte loads in flight per thread before any add (HBM latency, not the adds,
+    // bounds a dependent load chain)
+    int m = r0 + rl;
+    for (; m + 56 < r1; m += 64) {
+      bf8 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const bf8*>(x + (long long)(m + 8 * u) * ldx + col);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+    }
+    for (; m < r1; m += 8) {
       float f[8];
       unpack8(*reinterpret_cast<const bf8*>(x + (long long)m * ldx + col), f);
 #pragma unroll
@@ -298,8 +313,9 @@ OTAMD_API int otamd_upsample2x_bwd(const void* dup, void* dx, int N, int H, int 
 static int colsum_rpb(int rows_per_group, int N, int groups) {
   const int cblocks = (N + 255) / 256;
   int rpb = rows_per_group;
-  // ~512 first-pass blocks; each then streams >= 64 rows (8 per thread-row) and RB stays small
-  while (rpb > 256 && (long long)cblocks * groups * ((rows_per_group + rpb - 1) / rpb) < 512) rpb = (rpb + 1) / 2;
+  // ~2048 first-pass blocks (8 per CU) so enough loads are in flight to cover HBM latency; each block
+  // still streams >= 128 rows (16 per thread-row: two batches of 8 loads) and RB stays small
+  while (rpb > 128 && (long long)cblocks * groups * ((rows_per_group + rpb - 1) / rpb) < 2048) rpb = (rpb + 1) / 2;
   return rpb;
 }
 OTAMD_API long long otamd_colsum_ws_floats(int M, int N, int rows_per_group) {

@@ -1,0 +1,11 @@
+# One GPU call: kernel parity -> GEMM census (side stream off: isolated launch times) -> bench.
+# usage: bash tools/gpu_census.sh <tag>
+set -o pipefail
+TAG=${1:-census}
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_$TAG.log; exit 1; }
+tail -2 gpurun_out/pytest_$TAG.log
+OTAMD_WGRAD_STREAM=0 timeout -k 10 300 python -u tools/gemm_census.py --steps 2 > gpurun_out/census_$TAG.jsonl 2> gpurun_out/census_$TAG.err || { echo "census failed"; tail -30 gpurun_out/census_$TAG.err; exit 1; }
+timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-vae > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
