@@ -98,6 +98,7 @@ def gemm_roofline(tr, batch):
     from onetrainer_amd.module import streams
     was = streams.enabled()
     streams.set_enabled(False)   # per-launch durations in isolation (no side-stream overlap)
+    graphs, tr.graphs = tr.graphs, None   # an eager step: every GEMM launched (and timed) from the host
     K._gemm = timed
     try:
         tr.train_step(batch)
@@ -105,6 +106,7 @@ def gemm_roofline(tr, batch):
     finally:
         K._gemm = orig
         streams.set_enabled(was)
+        tr.graphs = graphs
     flops = sum(r[0] for r in recs)
     ms = sum(r[1].elapsed_time(r[2]) for r in recs)
     return flops, ms, len(recs)
@@ -117,9 +119,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 4 sdxl / 16 sd15)")
     ap.add_argument("--res", type=int, default=None, help="default 1024 (sdxl) / 512 (sd15)")
-    ap.add_argument("--model", choices=["sdxl", "sd15", "flux"], default="sdxl",
+    ap.add_argument("--model", choices=["sdxl", "sd15", "flux", "sdxl-lora"], default="sdxl",
                     help="sdxl: configs[2] per GPU (metric workload); sd15: configs[1] (SD 1.5 512^2 b=16); "
-                         "flux: configs[4] per GPU (FLUX.1 LoRA r16, 768^2, b=4)")
+                         "flux: configs[4] per GPU (FLUX.1 LoRA r16, 768^2, b=4); sdxl-lora: configs[3] per GPU "
+                         "(SDXL LoRA r32, aspect-ratio buckets drawn per step, b=4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true", help="skip the VAE-encode (latent caching) side measurement")
     ap.add_argument("--cpu-res", type=int, default=512)
@@ -135,6 +138,7 @@ def main():
 
     sd15 = args.model == "sd15"
     flux = args.model == "flux"
+    sdxl_lora = args.model == "sdxl-lora"
     if args.res is None:
         args.res = 512 if sd15 else (768 if flux else 1024)
     if args.batch is None:
@@ -147,8 +151,12 @@ def main():
         cfg.model_type, cfg.training_method = "FLUX_DEV_1", "LORA"
         cfg.timestep_distribution = "LOGIT_NORMAL"
         args.no_vae = True
+    if sdxl_lora:   # training_presets/#sdxl 1.0 LoRA.json (lr 3e-4) + lora_rank 32, fp32 adapters, ARB on
+        cfg.training_method = "LORA"
+        cfg.lora_rank = 32
+        args.no_vae = True
     cfg.batch_size = args.batch
-    cfg.learning_rate = 3e-6
+    cfg.learning_rate = 3e-4 if sdxl_lora else 3e-6
     cfg.learning_rate_warmup_steps = 0
     cfg.resolution = str(args.res)
 
@@ -165,12 +173,24 @@ def main():
     if flux:
         from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_flux_batch
         batch = synthetic_flux_batch(args.batch, args.res, args.res, dev, seed=rank)
+    elif sdxl_lora:
+        # every step draws ONE bucket for the whole global batch (seeded, identical
+        # on all ranks, §8(e)); buckets of the restated mgds AspectBucketing, aspects up to 1:1.75
+        import random
+        from onetrainer_amd.dataLoader.aspect_bucketing import ASPECTS, AspectBucketing
+        buckets = AspectBucketing(args.res, 64, ASPECTS[:4]).resolutions
+        arb = {r: synthetic_sdxl_batch(args.batch, r[0], r[1], dev, seed=rank) for r in buckets}
+        order = [random.Random(1000 + i).choice(buckets) for i in range(args.warmup + args.steps + 1)]
     else:
         batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=rank, sdxl=not sd15,
                                      scaling_factor=0.18215 if sd15 else 0.13025)
+    if sdxl_lora:
+        for r in buckets:   # every bucket shape once (plans, workspaces), untimed
+            tr.train_step(arb[r])
+        batch = arb[buckets[0]]
 
     for i in range(args.warmup):
-        tr.train_step(batch)
+        tr.train_step(arb[order[i]] if sdxl_lora else batch)
         if i == 0:
             torch.cuda.synchronize()
             log(f"[bench] first step done, mem {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
@@ -184,7 +204,7 @@ def main():
     evs[0].record(stream)
     losses = []
     for i in range(args.steps):
-        losses.append(tr.train_step(batch))
+        losses.append(tr.train_step(arb[order[args.warmup + i]] if sdxl_lora else batch))
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -222,6 +242,12 @@ def main():
         lora_tf = 2.0 * FX.lora_macs_per_image(tr.model.transformer_lora, 77, n_img) / 1e12
         train_tf_img = 2.0 * fwd_tf + 3.0 * lora_tf
         basis = f"{train_tf_img:.3f} TFLOP/image algorithmic (2 x {fwd_tf:.3f} base fwd + 3 x {lora_tf:.3f} LoRA)"
+    elif sdxl_lora:   # 2 x base forward (fwd + dgrad; frozen base) averaged over the drawn buckets
+        steps_b = order[args.warmup:args.warmup + args.steps]
+        fwd_tf = sum(flops_per_image(ucfg, h // 8, w // 8) for h, w in steps_b) / len(steps_b) / 1e12
+        train_tf_img = 2.0 * fwd_tf
+        basis = (f"{train_tf_img:.3f} TFLOP/image algorithmic (2 x {fwd_tf:.3f} base fwd averaged over the drawn "
+                 f"buckets; the LoRA branch GEMMs are not counted: conservative)")
     else:
         fwd_tf = flops_per_image(ucfg, args.res // 8, args.res // 8) / 1e12
         train_tf_img = 3.0 * fwd_tf                       # fwd + dgrad + wgrad
@@ -231,6 +257,11 @@ def main():
     label = "SD1.5 512^2 bf16" if sd15 else "SDXL 1024^2 bf16"
     wl = f"{'SD 1.5' if sd15 else 'SDXL 1.0'} UNet full fine-tune train step {args.res}^2 (latent {args.res // 8}^2), " \
          f"b={args.batch}/GPU, AdamW+bf16 SR, clip 1.0"
+    if sdxl_lora:
+        mname = "SDXL 1.0 UNet (2.567B params, bf16 frozen base) + LoRA r32 (every Linear/Conv2d, fp32)"
+        label = "SDXL LoRA r32 ARB ~1024^2 bf16"
+        wl = f"SDXL 1.0 LoRA rank 32 train step, aspect-ratio buckets {buckets} (one per step, seeded), " \
+             f"b={args.batch}/GPU, fp32 AdamW, clip 1.0"
     if flux:
         mname = "FLUX.1-dev transformer (11.9B params, bf16 base) + LoRA r16 (all Linear)"
         label = f"FLUX.1 LoRA {args.res}^2 bf16"
@@ -266,8 +297,10 @@ def main():
         "vae_encode": vae,
         "gemm_plans": "autotuned in warm-up (%d signatures)" % len(K.gemm_autotune_cache()) if args.autotune
         else "analytic",
+        "step_graph": (f"forward+backward replayed as HIP graphs ({len(tr.graphs.entries)} captured shapes); "
+                       f"noise/timesteps and the optimizer update eager") if tr.graphs is not None else "eager",
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not flux:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not flux and not sdxl_lora:
         del tr
         torch.cuda.empty_cache()
         log("[bench] cpu baseline (oracle, fp32) ...")

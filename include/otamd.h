@@ -199,6 +199,12 @@ int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, long long 
     lddx, int rows, int C, const void* gamma, const float* mean, const float* rstd, void* dgamma, void* dbeta,
     int param_f32, int param_acc, float* part, int accumulate, hipStream_t stream);
 
+/* replaces: the LayerNorm weight / bias gradient half of the same autograd node (dgamma = sum dy xhat,
+   dbeta = sum dy), issued separately so it can run on the weight-gradient side stream */
+int otamd_layernorm_param_grad(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,
+    const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32, int param_acc, float* part,
+    hipStream_t stream);
+
 /* replaces: diffusers GEGLU (ff.net.0) hidden * gelu(gate) */
 int otamd_geglu_fwd(const void* h, long long ldh, void* out, long long ldo, int M, int F, hipStream_t s);
 

@@ -700,18 +700,34 @@ __global__ void __launch_bounds__(512) ln_param_part_kernel(const bf16_t* __rest
 #pragma unroll
   for (int j = 0; j < 8; ++j) { dg[j] = 0.f; db[j] = 0.f; }
   if (ok) {
-#pragma unroll 4
-    for (long long r = r0 + w; r < r1; r += 8) {
+    auto body = [&](const bf8& xv, const bf8& dvv, float m, float rs) {
       float xf[8], dv[8];
-      unpack8(*reinterpret_cast<const bf8*>(x + r * ldx + c8 * 8), xf);
-      unpack8(*reinterpret_cast<const bf8*>(dy + r * lddy + c8 * 8), dv);
-      const float m = mean_in[r], rs = rstd_in[r];
+      unpack8(xv, xf);
+      unpack8(dvv, dv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         dg[j] = fmaf(dv[j], (xf[j] - m) * rs, dg[j]);
         db[j] += dv[j];
       }
+    };
+    long long r = r0 + w;
+    // 4 rows (8 independent 16-byte loads) in flight per lane before any math
+    for (; r + 24 < r1; r += 32) {
+      bf8 xv[4], dv[4];
+      float m[4], rs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xv[u] = *reinterpret_cast<const bf8*>(x + (r + 8 * u) * ldx + c8 * 8);
+        dv[u] = *reinterpret_cast<const bf8*>(dy + (r + 8 * u) * lddy + c8 * 8);
+        m[u] = mean_in[r + 8 * u];
+        rs[u] = rstd_in[r + 8 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) body(xv[u], dv[u], m[u], rs[u]);
     }
+    for (; r < r1; r += 8)
+      body(*reinterpret_cast<const bf8*>(x + r * ldx + c8 * 8), *reinterpret_cast<const bf8*>(dy + r * lddy + c8 * 8),
+           mean_in[r], rstd_in[r]);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[w][0][j][lane] = dg[j]; red[w][1][j][lane] = db[j]; }
@@ -757,6 +773,10 @@ __global__ void __launch_bounds__(1024) ln_param_reduce2_kernel(const float* __r
     if (c < C) store_param_grad(dgamma, c, t, pf32, pacc); else store_param_grad(dbeta, c - C, t, pf32, pacc);
   }
 }
+
+static int ln_param_grads(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,
+                          const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32,
+                          int param_acc, float* part, hipStream_t stream);
 
 OTAMD_API int otamd_layernorm_fwd(const void* x, long long ldx, void* y, long long ldy, int rows, int C, float eps,
                                   const void* gamma, const void* beta, float* mean, float* rstd, hipStream_t stream) {
@@ -818,19 +838,7 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
 #undef LNB
     OTAMD_CHECK_LAUNCH();
     if (!dgamma) return OTAMD_OK;
-    // row slabs of >= 64 rows, at most 512 (the part buffer holds 1024 x 2C floats)
-    const int cb = (C / 8 + 63) / 64;
-    int slabs = (rows + 63) / 64;
-    if (slabs > 512) slabs = 512;
-    if (slabs * cb < 1024 && slabs < (rows + 15) / 16) slabs = min((rows + 15) / 16, min(512, 1024 / cb));
-    const int rps = (rows + slabs - 1) / slabs;
-    slabs = (rows + rps - 1) / rps;
-    ln_param_part_kernel<<<dim3(cb, slabs), 512, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, rows, C,
-                                                              mean, rstd, rps, part);
-    OTAMD_CHECK_LAUNCH();
-    ln_param_reduce2_kernel<<<(2 * C + 63) / 64, 1024, 0, stream>>>(part, slabs, C, dgamma, dbeta, param_f32, param_acc);
-    OTAMD_CHECK_LAUNCH();
-    return OTAMD_OK;
+    return ln_param_grads(x, ldx, dy, lddy, rows, C, mean, rstd, dgamma, dbeta, param_f32, param_acc, part, stream);
   }
   int nb = (rows + 3) / 4;
   if (nb > 512) nb = 512;
@@ -842,4 +850,38 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
   ln_param_reduce_kernel<<<(2 * C + 31) / 32, 256, 0, stream>>>(part, nb, C, dgamma, dbeta, param_f32, param_acc);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
+}
+
+// dgamma / dbeta only (the dx pass ran with dgamma == nullptr): lets the parameter-gradient reduction
+// run on the weight-gradient side stream, off the critical dgrad chain (module/streams.py).
+// part: float scratch >= 1024 * 2 * C
+OTAMD_API int otamd_layernorm_param_grad(const void* x, long long ldx, const void* dy, long long lddy, int rows,
+                                         int C, const float* mean, const float* rstd, void* dgamma, void* dbeta,
+                                         int param_f32, int param_acc, float* part, hipStream_t stream) {
+  if (!x || !dy || !mean || !rstd || !dgamma || !dbeta || !part) return OTAMD_EINVAL;
+  if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8) return OTAMD_EINVAL;
+  if (((uintptr_t)x | (uintptr_t)dy) & 15) return OTAMD_EINVAL;
+  return ln_param_grads(x, ldx, dy, lddy, rows, C, mean, rstd, dgamma, dbeta, param_f32, param_acc, part, stream);
+}
+
+static int ln_param_grads(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,
+                          const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32,
+                          int param_acc, float* part, hipStream_t stream) {
+  {
+    // ~256 blocks (one per CU) of >= 32 rows (4 per wave, one unrolled batch), at most 512 slabs (the
+    // part buffer holds 1024 x 2C floats): few slabs keep the second (reduce) pass short -- with
+    // 16-row slabs both passes were latency-bound (~11 us + ~8.5 us per LayerNorm at 4096 x 1280)
+    const int cb = (C / 8 + 63) / 64;
+    int slabs = (256 + cb - 1) / cb;
+    slabs = min(slabs, max(1, rows / 32));
+    slabs = min(slabs, 512);
+    const int rps = (rows + slabs - 1) / slabs;
+    slabs = (rows + rps - 1) / rps;
+    ln_param_part_kernel<<<dim3(cb, slabs), 512, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, rows, C,
+                                                              mean, rstd, rps, part);
+    OTAMD_CHECK_LAUNCH();
+    ln_param_reduce2_kernel<<<(2 * C + 63) / 64, 1024, 0, stream>>>(part, slabs, C, dgamma, dbeta, param_f32, param_acc);
+    OTAMD_CHECK_LAUNCH();
+    return OTAMD_OK;
+  }
 }

@@ -487,6 +487,19 @@ def layernorm_bwd(x, dy, gamma, stats, dx=None, accumulate=False, dgamma=None, d
     return dx, dgamma, dbeta
 
 
+def layernorm_param_grad(x, dy, stats, dgamma, dbeta, param_acc=False):
+    """dgamma += / = sum_rows dy * xhat, dbeta = sum_rows dy (bf16 or f32 destinations)."""
+    rows, C_, ldx = _rows2d(x)
+    _, _, lddy = _rows2d(dy)
+    _req(dgamma.dtype == dbeta.dtype and dgamma.dtype in (BF16, F32), "layernorm param grads bf16 / f32")
+    part = workspace(1024 * 2 * C_ * 4, x.device)
+    mean, rstd = stats
+    check(lib().otamd_layernorm_param_grad(_p(x), ldx, _p(dy), lddy, rows, C_, _p(mean), _p(rstd), _p(dgamma),
+                                           _p(dbeta), int(dgamma.dtype == F32), int(param_acc), _p(part),
+                                           stream_handle()), "otamd_layernorm_param_grad")
+    return dgamma, dbeta
+
+
 # ------------------------------------------------------------------------------------------
 # attention: q [B, Nq, H*D] views (token stride = row stride), k/v [B, Nk, H*D]
 def _attn_view(t: torch.Tensor, heads: int):
@@ -797,16 +810,20 @@ def add(a, b, out=None):
 
 # ------------------------------------------------------------------------------------------
 # diffusion step kernels
-def noise(shape, seed, offset=0, dtype=BF16, device=None):
-    out = torch.empty(shape, dtype=dtype, device=device)
+def noise(shape, seed, offset=0, dtype=BF16, device=None, out=None):
+    if out is None:
+        out = torch.empty(shape, dtype=dtype, device=device)
+    _req(tuple(out.shape) == tuple(shape) and out.dtype == dtype and out.is_contiguous(), "noise out")
     check(lib().otamd_noise(_p(out), int(dtype == F32), out.numel(), offset, seed & 0xFFFFFFFFFFFFFFFF,
                             stream_handle()), "otamd_noise")
     return out
 
 
 def timesteps(n, seed, sample0=0, dist=0, num_train_timesteps=1000, min_s=0.0, max_s=1.0, shift=1.0, bias=0.0,
-              weight=0.0, device=None):
-    out = torch.empty(n, dtype=torch.int32, device=device)
+              weight=0.0, device=None, out=None):
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=device)
+    _req(out.numel() == n and out.dtype == torch.int32 and out.is_contiguous(), "timesteps out")
     check(lib().otamd_timesteps(_p(out), n, sample0, seed & 0xFFFFFFFFFFFFFFFF, dist, num_train_timesteps,
                                 float(min_s), float(max_s), float(shift), float(bias), float(weight), stream_handle()),
           "otamd_timesteps")

@@ -29,6 +29,7 @@ class BaseStableDiffusionXLSetup:
         self.debug_mode = debug_mode
         self.dp_rank = dp_rank
         self.dp_world = dp_world
+        self.graph_inputs = None   # (noise, timestep) drawn outside a captured step (trainer/step_graph.py)
 
     # ------------------------------------------------------------------------------------------
     @staticmethod
@@ -54,6 +55,38 @@ class BaseStableDiffusionXLSetup:
                                                         te2.to(torch.bfloat16), pooled)
         return ehs, pooled
 
+    def graphable(self, config) -> bool:
+        """the step has no host-random or host-varying input besides (noise, timestep), so it can be
+        captured once and replayed (text dropout draws its mask on the host per step)."""
+        parts = [config.text_encoder] + ([config.text_encoder_2] if hasattr(config, "text_encoder_2") else [])
+        return (config.offset_noise_weight <= 0 and config.perturbation_noise_weight <= 0
+                and all(not (p.dropout_probability or 0) > 0 for p in parts))
+
+    def step_inputs(self, model, batch: dict, config, train_progress, *, deterministic: bool = False, out=None):
+        """(noise, timestep) of this micro-step (ModelSetupNoiseMixin._create_noise /
+        _get_timestep_discrete): Philox seeded by `batch_seed`, counter = GLOBAL batch index."""
+        batch_seed = 0 if deterministic else train_progress.global_step
+        lat = batch["latent_image"]
+        B = lat.shape[0]
+        shape = tuple(self._nhwc_latent(lat).shape) if out is None else tuple(out[0].shape)
+        _, h, w, C = shape
+        sample0 = self.dp_rank * B                       # global-batch index of this rank's first sample
+        noise = K.noise(shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=lat.dtype, device=lat.device,
+                        out=None if out is None else out[0])
+        N = model.noise_scheduler.config["num_train_timesteps"]
+        if deterministic:
+            timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=lat.device)
+            if out is not None:
+                timestep = out[1].copy_(timestep)
+        else:
+            dist = {"UNIFORM": 0, "LOGIT_NORMAL": 1}[config.timestep_distribution]
+            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=dist, num_train_timesteps=N,
+                                   min_s=config.min_noising_strength, max_s=config.max_noising_strength,
+                                   shift=config.timestep_shift, bias=config.noising_bias,
+                                   weight=config.noising_weight, device=lat.device,
+                                   out=None if out is None else out[1])
+        return noise, timestep
+
     def predict(self, model, batch: dict, config, train_progress, *, deterministic: bool = False) -> dict:
         if config.offset_noise_weight > 0 or config.perturbation_noise_weight > 0:
             raise NotImplementedError("offset / perturbation noise are not on this build's hot path yet")
@@ -63,18 +96,10 @@ class BaseStableDiffusionXLSetup:
         B, h, w, C = latent.shape
         sf = model.vae.config["scaling_factor"]
         ehs, pooled = self._text(model, batch, config, rand, B)
-        sample0 = self.dp_rank * B                       # global-batch index of this rank's first sample
-        noise = K.noise(latent.shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=latent.dtype,
-                        device=latent.device)
-        N = model.noise_scheduler.config["num_train_timesteps"]
-        if deterministic:
-            timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=latent.device)
+        if self.graph_inputs is not None:
+            noise, timestep = self.graph_inputs
         else:
-            dist = {"UNIFORM": 0, "LOGIT_NORMAL": 1}[config.timestep_distribution]
-            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=dist, num_train_timesteps=N,
-                                   min_s=config.min_noising_strength, max_s=config.max_noising_strength,
-                                   shift=config.timestep_shift, bias=config.noising_bias,
-                                   weight=config.noising_weight, device=latent.device)
+            noise, timestep = self.step_inputs(model, batch, config, train_progress, deterministic=deterministic)
         ptype = model.noise_scheduler.config["prediction_type"]
         unet_in, target, _ = K.ddpm_prologue(latent, noise, timestep, model.noise_scheduler.coeffs, sf,
                                              1 if ptype == "v_prediction" else 0)

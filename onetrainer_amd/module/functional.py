@@ -308,9 +308,10 @@ class LayerNormFn(torch.autograd.Function):
         if dy.stride(-1) != 1:
             dy = dy.contiguous()
         tr = ctx.gref.trainable
-        dx, _, _ = K.layernorm_bwd(x, dy, ctx.gref.w, stats, dgamma=ctx.gref.g if tr else None,
-                                   dbeta=ctx.bref.g if tr else None, param_acc=tr and ctx.gref.acc(),
-                                   need_param_grads=tr)
+        if tr:   # dgamma / dbeta only feed the optimizer: side stream, like the GEMM weight gradients
+            with S.wgrad_region((x, dy, *stats)):
+                K.layernorm_param_grad(x, dy, stats, ctx.gref.g, ctx.bref.g, param_acc=ctx.gref.acc())
+        dx, _, _ = K.layernorm_bwd(x, dy, ctx.gref.w, stats, need_param_grads=False)
         if tr:
             ctx.gref.done()
             ctx.bref.done()

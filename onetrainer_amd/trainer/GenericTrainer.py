@@ -8,7 +8,9 @@ Differences, all MI355X-motivated and semantics-preserving:
   * no per-step host sync: the reference calls loss.item() every step (line 699); here the loss
     stays on device and is read every `log_every` steps;
   * the global clip runs on device and is applied inside the fused AdamW launch;
-  * data parallel (new): gradient buckets are all-reduced from inside backward (trainer/ddp.py).
+  * data parallel (new): gradient buckets are all-reduced from inside backward (trainer/ddp.py);
+  * single-GPU, opt-in (OTAMD_STEP_GRAPH=1): forward + backward captured once per batch shape and
+    replayed as one HIP graph (trainer/step_graph.py; measured slower than the two-stream eager step).
 start()/train()/end() keep the reference's external behaviour (scripts/train.py:32-43).
 """
 from __future__ import annotations
@@ -35,6 +37,7 @@ class GenericTrainer:
         self.seed = seed
         self.lr_scheduler = None
         self.reducer = None
+        self.graphs = None
         self.loss_history: list[torch.Tensor] = []
 
     # ------------------------------------------------------------------------------------------
@@ -58,6 +61,9 @@ class GenericTrainer:
                                                 cfg.learning_rate_min_factor, cfg.epochs, approx,
                                                 cfg.gradient_accumulation_steps,
                                                 self.model.train_progress.global_step)
+        from .step_graph import StepGraphs
+        if StepGraphs.enabled_for(self):
+            self.graphs = StepGraphs(self)
 
     def _load_weights(self):
         """base / VAE / LoRA weights and a backup to continue from (GenericTrainer.py:92-108 +
@@ -149,12 +155,14 @@ class GenericTrainer:
         cfg, model, setup = self.config, self.model, self.model_setup
         tp = model.train_progress
         store = model.train_store
-        out = setup.predict(model, batch, cfg, tp)
-        loss = setup.calculate_loss(model, batch, out, cfg)
-        loss = loss / cfg.gradient_accumulation_steps
-        store.begin_backward()
-        loss.backward()
-        store.finish_backward()
+        loss = self.graphs.forward_backward(batch) if self.graphs is not None else None
+        if loss is None:   # eager (or the first sight of a shape before its capture: trainer/step_graph.py)
+            out = setup.predict(model, batch, cfg, tp)
+            loss = setup.calculate_loss(model, batch, out, cfg)
+            loss = loss / cfg.gradient_accumulation_steps
+            store.begin_backward()
+            loss.backward()
+            store.finish_backward()
         if self._is_update_step(tp):
             if self.reducer is not None:
                 self.reducer.finish()

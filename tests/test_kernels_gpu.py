@@ -40,7 +40,8 @@ def test_groupnorm(dev, N, H, W, C, G, silu, eps):
     assert rel_err(db, br.grad) < 1e-2
 
 
-@pytest.mark.parametrize("rows,C", [(4096, 640), (1000, 1280), (77, 320)])
+@pytest.mark.parametrize("rows,C", [(4096, 640), (1000, 1280), (77, 320), (16384, 640), (4096, 1280), (31, 1280),
+                                    (2381, 1536)])
 def test_layernorm(dev, rows, C):
     torch.manual_seed(1)
     x = rnd(rows, C, dev=dev, scale=3.0, shift=1.0)
@@ -55,6 +56,14 @@ def test_layernorm(dev, rows, C):
     assert rel_err(dx, xr.grad) < 2e-2
     assert rel_err(dg, gr.grad) < 1e-2
     assert rel_err(db, br.grad) < 1e-2
+    # the parameter-gradient half alone (side-stream form), bf16 destinations, then accumulated
+    dx2, none_g, _ = K.layernorm_bwd(x, dy, g, st, need_param_grads=False)
+    assert none_g is None and torch.equal(dx2, dx)
+    pg, pb = torch.zeros(C, dtype=BF, device=dev), torch.zeros(C, dtype=BF, device=dev)
+    K.layernorm_param_grad(x, dy, st, pg, pb)
+    assert rel_err(pg, gr.grad) < 1e-2 and rel_err(pb, br.grad) < 1e-2
+    K.layernorm_param_grad(x, dy, st, pg, pb, param_acc=True)
+    assert rel_err(pg, 2 * gr.grad) < 1e-2 and rel_err(pb, 2 * br.grad) < 1e-2
 
 
 def sdpa_ref(q, k, v, heads):

@@ -119,3 +119,36 @@ def test_dp_noise_slices_match_global(dev):
     s1 = BaseStableDiffusionXLSetup(dev, dp_rank=1, dp_world=2)
     off = s1.dp_rank * 2 * 16 * 16 * 4
     assert torch.equal(K.noise((2, 16, 16, 4), seed=9, offset=off, dtype=torch.float32, device=dev), g[2:])
+
+
+def test_step_graph_matches_eager(dev, monkeypatch):
+    """the captured + replayed step (trainer/step_graph.py) is bit-identical to the eager step:
+    losses, every parameter and the AdamW moments over 4 steps, with a second batch shape in the
+    middle (its own capture, sharing the graph memory pool)."""
+    ucfg = U.tiny_sdxl_config()
+
+    def run(graphs: bool):
+        monkeypatch.setenv("OTAMD_STEP_GRAPH", "1" if graphs else "0")   # opt-in
+        cfg = TrainConfig.default_values()
+        cfg.batch_size = 2
+        cfg.learning_rate = 1e-4
+        cfg.learning_rate_warmup_steps = 0
+        model = create.create_model(cfg, dev, seed=3, unet_config=ucfg)
+        tr = GenericTrainer(cfg, model=model)
+        tr.start()
+        assert (tr.graphs is not None) == graphs
+        a = synthetic_sdxl_batch(2, 128, 128, dev, seed=1, te1_dim=48, te2_dim=48, pooled_dim=64)
+        b = synthetic_sdxl_batch(2, 96, 160, dev, seed=2, te1_dim=48, te2_dim=48, pooled_dim=64)
+        a2 = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in a.items()}   # same shape, other buffers
+        losses = [tr.train_step(x).clone() for x in (a, a, b, b, a2, b, a)]
+        torch.cuda.synchronize()
+        opt = model.optimizer
+        return (torch.stack(losses).cpu(), model.unet.store.data.clone(),
+                torch.cat([opt.exp_avg.float(), opt.exp_avg_sq.float()]), tr)
+
+    l0, p0, s0, _ = run(False)
+    l1, p1, s1, tr1 = run(True)
+    assert len(tr1.graphs.entries) == 2
+    assert torch.equal(l0, l1), (l0, l1)
+    assert torch.equal(p0, p1)
+    assert torch.equal(s0, s1)

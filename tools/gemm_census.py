@@ -28,10 +28,13 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--lora", type=int, default=0, help="LoRA rank (0: full fine-tune)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = TrainConfig.default_values()
     cfg.batch_size = args.batch
+    if args.lora:
+        cfg.training_method, cfg.lora_rank = "LORA", args.lora
     model = create.create_model(cfg, dev, seed=0)
     tr = GenericTrainer(cfg, model=model)
     tr.start()
