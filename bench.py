@@ -93,7 +93,7 @@ def gemm_roofline(tr, batch):
         e0.record()
         orig(a, splits, device)
         e1.record()
-        recs.append((2.0 * a.M * a.N * a.K, e0, e1))
+        recs.append((2.0 * a.M * a.N * a.K, e0, e1, 2.0 * (a.M * a.K + a.K * a.N + a.M * a.N)))
 
     from onetrainer_amd.module import streams
     was = streams.enabled()
@@ -109,7 +109,18 @@ def gemm_roofline(tr, batch):
         tr.graphs = graphs
     flops = sum(r[0] for r in recs)
     ms = sum(r[1].elapsed_time(r[2]) for r in recs)
+    gemm_roofline.algo_bytes = sum(r[3] for r in recs)   # GEMM-form operand bytes (conv A as im2col)
     return flops, ms, len(recs)
+
+
+def pmc_traffic():
+    """GEMM-family memory-side traffic per step from the committed PMC passes (tools/gpu_pmc.sh:
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs, FETCH_SIZE doubled for gfx950)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_sdxl1024_b4.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
 
 
 def main():
@@ -231,6 +242,7 @@ def main():
         from tools.bench_vae import run as vae_run
         vae = vae_run(args.res, args.batch, iters=5, warmup=1, device=str(dev))
     g_achieved = g_flops / (g_ms * 1e-3) / 1e12
+    pmc = pmc_traffic()
 
     imgs = args.batch * world * args.steps
     value = imgs / elapsed
@@ -287,7 +299,11 @@ def main():
                    "seq_len": (args.res // 8) ** 2, "parallelism": f"dp{world}"},
         "loss": round(loss_val, 5),
         "roofline": {"bound": "mfma", "achieved": round(g_achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(g_achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(g_achieved / PEAK_BF16_TFLOPS, 4),
+                     "traffic": (pmc["gemm_total_gb"] if pmc and not (sd15 or flux or sdxl_lora) else None),
+                     "traffic_unit": "GB per step, GEMM family (FETCH_SIZE x 2 + WRITE_SIZE, memory-side L2 counters: "
+                                     "Infinity-Cache hits included), from profiles/pmc_traffic_sdxl1024_b4.json",
+                     "algorithmic_gb": round(gemm_roofline.algo_bytes / 1e9, 2),
                      "kernel": "bf16 MFMA GEMM / implicit-GEMM conv (gemm2_kernel<*>, gemm_kernel, splitk_reduce_kernel)",
                      "basis": f"sum(2*M*N*K) over the {g_n} GEMM/conv launches of one step / sum of their HIP-event "
                               f"durations ({g_ms:.2f} ms of GEMM per step)",

@@ -385,21 +385,36 @@ static int forced_tile() {
       else if (!strcmp(e, "256x128")) forced = 1;
       else if (!strcmp(e, "128x256")) forced = 2;
       else if (!strcmp(e, "256x256w4")) forced = 3;
+      else if (!strcmp(e, "128x128w8")) forced = 4;
     }
   }
   return forced;
 }
 
+// candidate tiles of the analytic plan: (tile code, BM, BN, workgroups per CU, relative per-CU
+// throughput, fixed prologue/epilogue seconds).  Tile 4 (128x128, 8 waves, 2 workgroups per CU) has
+// the smallest epilogue and fills the chip on the 4096-row SDXL level-2 shapes where 256-wide tiles
+// leave CUs idle (tools/gemm_tiles.py on MI355X: 4096x1280x1280 30.3 -> 26.2 us, 4096x10240x1280
+// 129.5 -> 114.2 us, 4096x5120x1280 69.0 -> 60.0 us).
+struct TileCand { int tile, bm, bn, per_cu; double rate, fixed; };
+static const TileCand kTiles[5] = {{-1, 128, 128, 2, 0.55, 2.5e-6}, {0, 256, 256, 1, 1.0, 2.5e-6},
+                                   {1, 256, 128, 1, 0.85, 2.5e-6}, {2, 128, 256, 1, 0.85, 2.5e-6},
+                                   {4, 128, 128, 2, 0.85, 0.6e-6}};
+
+static bool no_tile4() {   // OTAMD_GEMM_NO_T4=1: plan without the 128x128 tile (A/B measurements)
+  static const bool v = getenv("OTAMD_GEMM_NO_T4") && !strcmp(getenv("OTAMD_GEMM_NO_T4"), "1");
+  return v;
+}
+
 static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = false) {
-  const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, per_cu[4] = {2, 1, 1, 1};
-  const double rate[4] = {0.55, 1.0, 0.85, 0.85};
   const double cu_flops = 1.1e15 / 256.0;    // effective per-CU rate of the 256x256 tile
   const int ft = forced_tile();
   GemmPlan best = {-1, 1};
   double best_t = 1e300;
-  for (int t = 0; t < 4; ++t) {
-    if (ft != -3 && t - 1 != ft) continue;
-    if (v2_only && t == 0) continue;
+  for (const TileCand& c : kTiles) {
+    if (ft != -3 && c.tile != ft) continue;
+    if (v2_only && c.tile < 0) continue;
+    if (c.tile == 4 && ft == -3 && no_tile4()) continue;
     int prev_se = 0;
     for (int s = 1; s <= max_splits; ++s) {   // every split count (3 and 5 often fill the chip best)
       const long long kps = ((long long)(K + s - 1) / s + 63) / 64 * 64;
@@ -407,13 +422,16 @@ static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = fa
       const int se = (int)((K + kps - 1) / kps);
       if (se == prev_se) continue;
       prev_se = se;
-      const long long tiles = (long long)((M + bm[t] - 1) / bm[t]) * ((N + bn[t] - 1) / bn[t]) * se;
-      const long long slots = 256LL * per_cu[t];
+      // split plans are re-tiled by resolve_tile (otamd_gemm is always called with the planned
+      // splits), which keeps the 256-wide tiles: the 128x128 tile is an unsplit-only candidate
+      if (se > 1 && c.tile == 4) continue;
+      const long long tiles = (long long)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn) * se;
+      const long long slots = 256LL * c.per_cu;
       const long long waves = (tiles + slots - 1) / slots;
-      const double tile_t = 2.0 * bm[t] * bn[t] * (double)kps / (cu_flops * rate[t] / per_cu[t]);
-      double tt = waves * (tile_t + 2.5e-6);
+      const double tile_t = 2.0 * c.bm * c.bn * (double)kps / (cu_flops * c.rate / c.per_cu);
+      double tt = waves * (tile_t + c.fixed);
       if (se > 1) tt += ((double)se * M * N * 4.0 + (double)M * N * 2.0) / 4.5e12 + 3e-6;
-      if (tt < best_t * 0.98) { best_t = tt; best = {t - 1, se}; }
+      if (tt < best_t * 0.98) { best_t = tt; best = {c.tile, se}; }
     }
   }
   return best;
@@ -436,7 +454,7 @@ OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_
 static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_only);
 
 // the tile otamd_gemm would launch for these arguments and splits (0 = automatic): -1 = v1 128x128,
-// 0 = 256x256, 1 = 256x128, 2 = 128x256 (8 waves), 3 = 256x256 (4 waves)
+// 0 = 256x256, 1 = 256x128, 2 = 128x256 (8 waves), 3 = 256x256 (4 waves), 4 = 128x128 (8 waves)
 OTAMD_API int otamd_gemm_plan_tile(const GemmArgs* in, int splits) {
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -9;
   const bool v2_only = in->bmode == OPM_CONV_WT || in->A2 != nullptr;
@@ -452,12 +470,11 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
   if (splits > 1 && forced_tile() == -3) {
     tile = -1;
     double bt = 1e300;
-    const int bm[4] = {128, 256, 256, 128}, bn[4] = {128, 256, 128, 256}, pc[4] = {2, 1, 1, 1};
-    const double rate[4] = {0.55, 1.0, 0.85, 0.85};
-    for (int t = v2_only ? 1 : 0; t < 4; ++t) {
-      const long long tiles = (long long)((a.M + bm[t] - 1) / bm[t]) * ((a.N + bn[t] - 1) / bn[t]) * splits;
-      const double c = (double)((tiles + 256LL * pc[t] - 1) / (256LL * pc[t])) * bm[t] * bn[t] / rate[t] * pc[t];
-      if (c < bt * 0.98) { bt = c; tile = t - 1; }
+    for (const TileCand& c : kTiles) {
+      if ((v2_only && c.tile < 0) || c.tile == 4) continue;
+      const long long tiles = (long long)((a.M + c.bm - 1) / c.bm) * ((a.N + c.bn - 1) / c.bn) * splits;
+      const double cost = (double)((tiles + 256LL * c.per_cu - 1) / (256LL * c.per_cu)) * c.bm * c.bn / c.rate * c.per_cu;
+      if (cost < bt * 0.98) { bt = cost; tile = c.tile; }
     }
   } else if (forced_tile() != -3) {
     tile = forced_tile();
@@ -540,10 +557,11 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
 }
 
 // explicit plan (the autotuner's candidates and its cached choice): tile -1 = v1 128x128, 0 = 256x256,
-// 1 = 256x128, 2 = 128x256, 3 = 256x256 (4 waves); splits >= 1 (rounded to whole 64-deep K steps)
+// 1 = 256x128, 2 = 128x256, 3 = 256x256 (4 waves), 4 = 128x128 (8 waves, 2 workgroups per CU);
+// splits >= 1 (rounded to whole 64-deep K steps)
 OTAMD_API int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                                   hipStream_t stream) {
-  if (tile < -1 || tile > 3 || splits < 1) return OTAMD_EINVAL;
+  if (tile < -1 || tile > 4 || splits < 1) return OTAMD_EINVAL;
   return gemm_impl(in, splits, tile, workspace, ws_bytes, stream);
 }
 

@@ -197,7 +197,7 @@ __device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
 // unified VGPR/AGPR file), 256x256 as 2x2 wave tiles of 128x128 -- a third less LDS read traffic
 // per MFMA (one 16x16x32 fragment read per 4 MFMAs instead of per 2.7).
 template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2>
-__global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
+__global__ void __launch_bounds__(NW * 64, (BM == 128 && BN == 128) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
                                                                  unsigned a2_bytes, unsigned b2_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int WN = NW == 4 ? 2 : ((BM == 256 && BN == 128) ? 2 : 4);
@@ -273,13 +273,17 @@ __global__ void __launch_bounds__(NW * 64, NW / 4) gemm2_kernel(GemmArgs args, u
       for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
   };
   // interleave the next fragment reads into the current MFMA block: {2 MFMA, reads of 1 fragment} x (MI+NJ)
+  // (128x128: 8 MFMAs per half for 6 fragment reads -> {1 MFMA, reads} x 6, then the rest)
+  constexpr int NR = MI + NJ;
+  constexpr int PER = (MI * NJ) / NR >= 2 ? 2 : 1;
+  constexpr int REST = MI * NJ - PER * NR;
   auto interleave = [&]() {
 #pragma unroll
-    for (int t = 0; t < MI + NJ; ++t) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    for (int t = 0; t < NR; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, AK && BKm ? 1 : 2, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ - 2 * (MI + NJ), 0);
+    if constexpr (REST > 0) __builtin_amdgcn_sched_group_barrier(0x008, REST, 0);
   };
 
   // Pipeline, ONE barrier per K-step:
@@ -421,6 +425,7 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   if (tile == 0) fn = pick2<256, 256, 8>(a.amode, a.bmode, seg2);
   else if (tile == 1) { fn = pick2<256, 128, 8>(a.amode, a.bmode, seg2); BNv = 128; }
   else if (tile == 2) { fn = pick2<128, 256, 8>(a.amode, a.bmode, seg2); BMv = 128; }
+  else if (tile == 4) { fn = pick2<128, 128, 8>(a.amode, a.bmode, seg2); BMv = 128; BNv = 128; }
   else if (!seg2) { fn = pick2<256, 256, 4>(a.amode, a.bmode, false); NWv = 4; }
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);

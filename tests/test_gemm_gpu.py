@@ -1,4 +1,6 @@
 """GEMM engine parity vs a plain PyTorch fp32 reference of the same op (GPU)."""
+import ctypes as C
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -131,6 +133,42 @@ def test_autotuned_plans(dev, autotune):
     n = len(K.gemm_autotune_cache())
     assert n >= 5
     for t, s in K.gemm_autotune_cache().values():
-        assert -1 <= t <= 3 and s >= 1
+        assert -1 <= t <= 4 and s >= 1
     K.linear(x, w, residual=r)           # cached: no new entries
     assert len(K.gemm_autotune_cache()) == n
+
+
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 4])
+def test_every_tile_explicit(dev, tile, monkeypatch):
+    """every engine tile (4 = 128x128 with 8 waves, 2 workgroups per CU) through otamd_gemm_explicit:
+    linear fwd (+bias +residual), dgrad, wgrad (split-K) and conv fwd / dgrad / wgrad, ragged sizes."""
+    torch.manual_seed(11)
+    splits = {"v": 1}
+
+    def explicit(a, s_, device):
+        sp = splits["v"]
+        ws_bytes = sp * a.M * a.N * 4 if sp > 1 else 0
+        ws = K.workspace(ws_bytes, device) if ws_bytes else None
+        rc = K.lib().otamd_gemm_explicit(C.byref(a), tile, sp, K._p(ws), ws_bytes, K.stream_handle())
+        if rc == 3 and tile in (-1, 3):   # OTAMD_EUNSUPPORTED: v1 has no conv-weight B, 4-wave tile has no 2nd segment
+            pytest.skip("tile unsupported for this operand form")
+        K.check(rc, "otamd_gemm_explicit")
+
+    monkeypatch.setattr(K, "_gemm", explicit)
+    x, w, b = rnd(1000, 640, dev=dev), rnd(328, 640, dev=dev, scale=0.05), rnd(328, dev=dev)
+    r = rnd(1000, 328, dev=dev)
+    close(K.linear(x, w, bias=b, residual=r), x.float() @ w.float().t() + b.float() + r.float())
+    dy = rnd(1000, 328, dev=dev)
+    close(K.linear_dgrad(dy, w), dy.float() @ w.float())
+    for sp in (1, 3):
+        splits["v"] = sp
+        close(K.linear_wgrad(dy, x), dy.float().t() @ x.float(), tol=1e-2)
+    splits["v"] = 1
+    xc = rnd(2, 24, 20, 64, dev=dev)
+    wc = rnd(96, 3, 3, 64, dev=dev, scale=0.05)
+    yc = K.conv2d(xc, wc, pad=1)
+    close(yc, to_nhwc(F.conv2d(nchw(xc), wc.permute(0, 3, 1, 2).float(), padding=1)))
+    if tile != -1:
+        dxc = K.conv2d_dgrad(yc, wc, (24, 20), 1, 1)
+        refd = torch.nn.grad.conv2d_input(nchw(xc).shape, wc.permute(0, 3, 1, 2).float(), nchw(yc), padding=1)
+        close(dxc, to_nhwc(refd))
