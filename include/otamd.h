@@ -199,6 +199,12 @@ int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, long long 
     lddx, int rows, int C, const void* gamma, const float* mean, const float* rstd, void* dgamma, void* dbeta,
     int param_f32, int param_acc, float* part, int accumulate, hipStream_t stream);
 
+/* replaces: autograd of LayerNorm + the autograd add of its input's second use as the block residual
+   (BasicTransformerBlock: norm1/2/3 input = to_out / ff residual): dx = LN_bwd(dy) + dres */
+int otamd_layernorm_bwd_res(const void* x, long long ldx, const void* dy, long long lddy, const void* dres,
+    long long ldres, void* dx, long long lddx, int rows, int C, const void* gamma, const float* mean,
+    const float* rstd, hipStream_t stream);
+
 /* replaces: the LayerNorm weight / bias gradient half of the same autograd node (dgamma = sum dy xhat,
    dbeta = sum dy), issued separately so it can run on the weight-gradient side stream */
 int otamd_layernorm_param_grad(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,

@@ -297,38 +297,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   }
 }
 
-// pairs[b,h,q] = {lse2, delta}, delta = sum_d dO * O  (fp32)
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, float2* __restrict__ pairs) {
-  const long long total = (long long)a.B * a.Nq * a.H;
-  const int lane = threadIdx.x & 63;
-  const int sub = lane & 7;    // 8 lanes per row, 8 elements each (Dv <= 64 per pass)
-  for (long long row = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / 8; row < total;
-       row += (long long)gridDim.x * blockDim.x / 8) {
-    const int hh = (int)(row % a.H);
-    const long long bq = row / a.H;
-    const int q = (int)(bq % a.Nq), b = (int)(bq / a.Nq);
-    const bf16_t* Op = a.o + b * a.bso + (long long)q * a.ldo + hh * a.Dv;
-    const bf16_t* Gp = a.dout + b * a.bsdo + (long long)q * a.lddo + hh * a.Dv;
-    float s = 0.f;
-    for (int d = sub * 8; d < a.Dv; d += 64) {
-      bf8 ov = *reinterpret_cast<const bf8*>(Op + d);
-      bf8 gv = *reinterpret_cast<const bf8*>(Gp + d);
-      float of[8], gf[8];
-      unpack8(ov, of);
-      unpack8(gv, gf);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s = fmaf(of[j], gf[j], s);
-    }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    if (sub == 0) {
-      const long long i = ((long long)b * a.H + hh) * a.Nq + q;
-      pairs[i] = make_float2(a.lse[i], s);
-    }
-  }
-}
-
 // dQ: per wave 32 queries, iterate over key tiles (K row + K transposed + V row images per stage)
 template <int D>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
@@ -361,15 +329,32 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   load_row_frags<D>(gf, a.dout + b * a.bsdo + hh * a.Dv, a.lddo, q0, a.Nq, a.Dv);
   const int q = q0 + r;
   const long long srow = ((long long)b * a.H + hh) * a.Nq;
-  const float2 pr = q < a.Nq ? reinterpret_cast<const float2*>(a.delta)[srow + q] : make_float2(0.f, 0.f);
+  // delta = sum_d dO * O for this lane's query (the two half-waves split the head dim), published
+  // with the forward's lse as the {lse, delta} pair the dK/dV kernel (launched next) streams: this
+  // replaces a separate delta pass over O and dO
+  float dlt = 0.f, lse2 = 0.f;
+  if (q < a.Nq) {
+    const bf16_t* Op = a.o + b * a.bso + (long long)q * a.ldo + hh * a.Dv;
+    const bf16_t* Gp = a.dout + b * a.bsdo + (long long)q * a.lddo + hh * a.Dv;
+    const int d1 = min(a.Dv, (h + 1) * (D / 2));
+    for (int d = h * (D / 2); d < d1; d += 8) {
+      float of[8], gv[8];
+      unpack8(*reinterpret_cast<const bf8*>(Op + d), of);
+      unpack8(*reinterpret_cast<const bf8*>(Gp + d), gv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt = fmaf(of[j], gv[j], dlt);
+    }
+    lse2 = a.lse[srow + q];
+  }
+  dlt += __shfl_xor(dlt, 32, 64);
+  if (h == 0 && q < a.Nq) reinterpret_cast<float2*>(const_cast<float*>(a.delta))[srow + q] = make_float2(lse2, dlt);
+  consume(dlt);
+  consume(lse2);
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < ntiles) issue(s, smem + s * STG);
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) { consume(qf[s]); consume(gf[s]); }
-  consume(pr.x);
-  consume(pr.y);
-  const float lse2 = pr.x, dlt = pr.y;
   const float c = a.scale * LOG2E;
   const f2v dl2 = {dlt, dlt};
 
@@ -658,17 +643,10 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   const int qsplit = attn_qsplit(a);
   a.qsplit = qsplit;
   if (ws_bytes < otamd_attn_bwd_ws_bytes(in)) return OTAMD_EINVAL;
-  float2* pairs = reinterpret_cast<float2*>(ws);
-  a.delta = ws;
+  a.delta = ws;   // {lse, delta} pairs: written by the dQ kernel, read by dK/dV
   if (qsplit > 1) {   // every slab element is written by exactly one block: no memset
     a.dk32 = ws + ((nrow * 2 + 64) / 64) * 64;
     a.dv32 = a.dk32 + (long long)qsplit * nkv;
-  }
-  {
-    long long threads = nrow * 8;
-    int blocks = (int)std::min<long long>((threads + 255) / 256, 8192);
-    attn_bwd_delta_kernel<<<blocks, 256, 0, stream>>>(a, pairs);
-    OTAMD_CHECK_LAUNCH();
   }
   const int kblocks = (a.Nk + 127) / 128;
   dim3 gq((a.Nq + 127) / 128, a.H, a.B);

@@ -634,7 +634,8 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ dx, long long lddx, int rows, int C,
                                                           const bf16_t* __restrict__ gamma,
                                                           const float* __restrict__ mean_in,
-                                                          const float* __restrict__ rstd_in, int accumulate, int L) {
+                                                          const float* __restrict__ rstd_in, int accumulate, int L,
+                                                          const bf16_t* __restrict__ res = nullptr, long long ldres = 0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & (L - 1), RPW = 64 / L;
   const long long row = ((long long)blockIdx.x * 4 + w) * RPW + lane / L;
@@ -670,12 +671,14 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(const bf16_t* __restri
     unpack8(xr[k], xf);
     unpack8(dr[k], dv);
     unpack8(*reinterpret_cast<const bf8*>(gamma + c8 * 8), gm);
-    float prev[8];
+    float prev[8], rg[8];
     if (accumulate) unpack8(*reinterpret_cast<const bf8*>(dx + row * lddx + c8 * 8), prev);
+    if (res) unpack8(*reinterpret_cast<const bf8*>(res + row * ldres + c8 * 8), rg);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       o[j] = rstd * (dv[j] * gm[j] - m1 - (xf[j] - mean) * rstd * m2);
       if (accumulate) o[j] += prev[j];
+      if (res) o[j] += rg[j];
     }
     *reinterpret_cast<bf8*>(dx + row * lddx + c8 * 8) = pack8(o);
   }
@@ -862,6 +865,37 @@ OTAMD_API int otamd_layernorm_param_grad(const void* x, long long ldx, const voi
   if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy) & 15) return OTAMD_EINVAL;
   return ln_param_grads(x, ldx, dy, lddy, rows, C, mean, rstd, dgamma, dbeta, param_f32, param_acc, part, stream);
+}
+
+// dx = LayerNorm-backward(dy) + dres in one pass: the LayerNorm input is also the block's residual
+// (BasicTransformerBlock norm1/2/3 + to_out / ff residual), so the two gradient contributions are
+// summed here instead of by a separate autograd add.  dgamma / dbeta: otamd_layernorm_param_grad.
+OTAMD_API int otamd_layernorm_bwd_res(const void* x, long long ldx, const void* dy, long long lddy, const void* dres,
+                                      long long ldres, void* dx, long long lddx, int rows, int C, const void* gamma,
+                                      const float* mean, const float* rstd, hipStream_t stream) {
+  if (!x || !dy || !dres || !dx || !gamma || !mean || !rstd) return OTAMD_EINVAL;
+  if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8 || lddx % 8 || ldres % 8) return OTAMD_EINVAL;
+  if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)dres | (uintptr_t)gamma) & 15) return OTAMD_EINVAL;
+  int L = 0;
+  const int cpl = ln_pick(C / 8, &L);
+  if (!cpl) return OTAMD_EUNSUPPORTED;
+  const int rpb = 4 * (64 / L);
+  const int nbr = (rows + rpb - 1) / rpb;
+#define LNBR(K) ln_bwd_rows_kernel<K><<<nbr, 256, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, \
+                                                               (bf16_t*)dx, lddx, rows, C, (const bf16_t*)gamma, mean, \
+                                                               rstd, 0, L, (const bf16_t*)dres, ldres)
+  switch (cpl) {
+    case 1: LNBR(1); break;
+    case 2: LNBR(2); break;
+    case 3: LNBR(3); break;
+    case 4: LNBR(4); break;
+    case 5: LNBR(5); break;
+    case 6: LNBR(6); break;
+    default: LNBR(8); break;
+  }
+#undef LNBR
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
 }
 
 static int ln_param_grads(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,

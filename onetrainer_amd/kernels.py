@@ -487,6 +487,24 @@ def layernorm_bwd(x, dy, gamma, stats, dx=None, accumulate=False, dgamma=None, d
     return dx, dgamma, dbeta
 
 
+def layernorm_bwd_res(x, dy, dres, gamma, stats):
+    """dx = LayerNorm-backward(dy) + dres (the input's gradient through its residual use), one pass."""
+    rows, C_, ldx = _rows2d(x)
+    _, _, lddy = _rows2d(dy)
+    _req(dres.shape == x.shape and dres.dtype == BF16, "layernorm residual grad: bf16, shape of x")
+    _, _, ldres = _rows2d(dres)
+    dx = torch.empty(x.shape, dtype=BF16, device=x.device)
+    _, _, lddx = _rows2d(dx)
+    mean, rstd = stats
+    rc = lib().otamd_layernorm_bwd_res(_p(x), ldx, _p(dy), lddy, _p(dres), ldres, _p(dx), lddx, rows, C_, _p(gamma),
+                                       _p(mean), _p(rstd), stream_handle())
+    if rc == 3:   # OTAMD_EUNSUPPORTED (width without a row-group form): two passes
+        layernorm_bwd(x, dy, gamma, stats, dx=dx, need_param_grads=False)
+        return add(dx, dres, out=dx)
+    check(rc, "otamd_layernorm_bwd_res")
+    return dx
+
+
 def layernorm_param_grad(x, dy, stats, dgamma, dbeta, param_acc=False):
     """dgamma += / = sum_rows dy * xhat, dbeta = sum_rows dy (bf16 or f32 destinations)."""
     rows, C_, ldx = _rows2d(x)

@@ -322,6 +322,45 @@ def layer_norm(x, gref, bref, eps=1e-5):
     return LayerNormFn.apply(x, gref, bref, eps, *_params(gref, bref))
 
 
+class LayerNormResFn(torch.autograd.Function):
+    """(LayerNorm(x), x) for a LayerNorm whose input is also the block's residual (diffusers
+    BasicTransformerBlock: norm1/2/3 input = the residual of attn1/attn2 to_out and ff.net.2).  The
+    second output aliases x; backward receives both gradient contributions and sums them inside the
+    LayerNorm-backward pass (otamd_layernorm_bwd_res) instead of leaving an autograd add."""
+
+    @staticmethod
+    def forward(ctx, x, gref, bref, eps, *params):
+        y, stats = K.layernorm_fwd(x, gref.w, bref.w, eps)
+        ctx.save_for_backward(x, *stats)
+        ctx.gref, ctx.bref = gref, bref
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        x, *stats = ctx.saved_tensors
+        if dy.stride(-1) != 1:
+            dy = dy.contiguous()
+        tr = ctx.gref.trainable
+        if tr:   # dgamma / dbeta only feed the optimizer: side stream
+            with S.wgrad_region((x, dy, *stats)):
+                K.layernorm_param_grad(x, dy, stats, ctx.gref.g, ctx.bref.g, param_acc=ctx.gref.acc())
+        if dres is None:
+            dx, _, _ = K.layernorm_bwd(x, dy, ctx.gref.w, stats, need_param_grads=False)
+        else:
+            if dres.stride(-1) != 1 or not dres.is_contiguous():
+                dres = dres.contiguous()
+            dx = K.layernorm_bwd_res(x, dy, dres, ctx.gref.w, stats)
+        if tr:
+            ctx.gref.done()
+            ctx.bref.done()
+        return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
+
+
+def layer_norm_res(x, gref, bref, eps=1e-5):
+    """-> (LayerNorm(x), residual alias of x); see LayerNormResFn."""
+    return LayerNormResFn.apply(x, gref, bref, eps, *_params(gref, bref))
+
+
 class SelfAttnFn(torch.autograd.Function):
     """qkv [B, N, 3C] (fused projection output) -> o [B, N, C]."""
 

@@ -312,19 +312,20 @@ class UNet2DConditionModel:
 
     def _block(self, h, p, C, heads, ehs):
         B, N, _ = h.shape
-        n1 = Fn.layer_norm(h, self.R(p + ".norm1.weight"), self.R(p + ".norm1.bias"))
+        # norm1/2/3 hand back their input as the residual alias: its two gradients meet in one pass
+        n1, h = Fn.layer_norm_res(h, self.R(p + ".norm1.weight"), self.R(p + ".norm1.bias"))
         wqkv = self.R([p + ".attn1.to_q.weight", p + ".attn1.to_k.weight", p + ".attn1.to_v.weight"], (3 * C, C))
         qkv = Fn.linear(n1, wqkv, lora=self._lo_fused([p + ".attn1.to_q", p + ".attn1.to_k", p + ".attn1.to_v"]))
         o = Fn.SelfAttnFn.apply(qkv, heads)
         h = self._linear(o, p + ".attn1.to_out.0", residual=h)
-        n2 = Fn.layer_norm(h, self.R(p + ".norm2.weight"), self.R(p + ".norm2.bias"))
+        n2, h = Fn.layer_norm_res(h, self.R(p + ".norm2.weight"), self.R(p + ".norm2.bias"))
         q = Fn.linear(n2, self.R(p + ".attn2.to_q.weight"), lora=self._lo(p + ".attn2.to_q"))
         ctxd = self.cfg.cross_attention_dim
         wkv = self.R([p + ".attn2.to_k.weight", p + ".attn2.to_v.weight"], (2 * C, ctxd))
         kv = Fn.linear(ehs, wkv, lora=self._lo_fused([p + ".attn2.to_k", p + ".attn2.to_v"]))
         o = Fn.CrossAttnFn.apply(q, kv, heads)
         h = self._linear(o, p + ".attn2.to_out.0", residual=h)
-        n3 = Fn.layer_norm(h, self.R(p + ".norm3.weight"), self.R(p + ".norm3.bias"))
+        n3, h = Fn.layer_norm_res(h, self.R(p + ".norm3.weight"), self.R(p + ".norm3.bias"))
         g = self._linear(n3, p + ".ff.net.0.proj")
         a = Fn.GEGLUFn.apply(g)
         return self._linear(a, p + ".ff.net.2", residual=h)

@@ -64,6 +64,9 @@ def test_layernorm(dev, rows, C):
     assert rel_err(pg, gr.grad) < 1e-2 and rel_err(pb, br.grad) < 1e-2
     K.layernorm_param_grad(x, dy, st, pg, pb, param_acc=True)
     assert rel_err(pg, 2 * gr.grad) < 1e-2 and rel_err(pb, 2 * br.grad) < 1e-2
+    # input gradient + the residual branch's gradient in one pass
+    dres = rnd(rows, C, dev=dev)
+    assert rel_err(K.layernorm_bwd_res(x, dy, dres, g, st), xr.grad + dres.float()) < 2e-2
 
 
 def sdpa_ref(q, k, v, heads):
