@@ -22,6 +22,8 @@
 // on the partial last tile, and the forward's O rescale skipped when no lane's max grew.
 #include "common.h"
 
+#include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_set>
 
@@ -298,12 +300,14 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 }
 
 // dQ: per wave 32 queries, iterate over key tiles (K row + K transposed + V row images per stage)
-template <int D>
+// NS = LDS ring depth.  D = 64 with NS = 2 (48 KiB) lets three blocks share a CU (150 VGPRs fit three
+// waves per SIMD), so the SDXL level-2 grid (8 x 20 heads x 4 = 640 blocks) runs in one round of
+// 768 slots instead of 1.25 rounds of 512 with NS = 3 (72 KiB).
+template <int D, int NS>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = KT * D * 2;
   constexpr int STG = 3 * TB;
-  constexpr int NS = 3;
   using RImg = DmaImg<D, KT, false>;
   using TImg = DmaImg<D, KT, true>;
   constexpr int LOADS = 2 * RImg::PW + TImg::PW;
@@ -651,11 +655,13 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   const int kblocks = (a.Nk + 127) / 128;
   dim3 gq((a.Nq + 127) / 128, a.H, a.B);
   dim3 gk(kblocks, a.H, a.B * qsplit);
+  static const bool dq3 = getenv("OTAMD_ATTN_DQ_NS3") && !strcmp(getenv("OTAMD_ATTN_DQ_NS3"), "1");   // A/B switch
   if (a.Dv <= 64) {
-    launch(attn_bwd_dq_kernel<64>, gq, 3 * 3 * KT * 64 * 2, stream, a);
+    if (dq3) launch(attn_bwd_dq_kernel<64, 3>, gq, 3 * 3 * KT * 64 * 2, stream, a);
+    else launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
     launch(attn_bwd_dkv_kernel<64>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);
   } else {
-    launch(attn_bwd_dq_kernel<128>, gq, 3 * 3 * KT * 128 * 2, stream, a);
+    launch(attn_bwd_dq_kernel<128, 3>, gq, 3 * 3 * KT * 128 * 2, stream, a);
     launch(attn_bwd_dkv_kernel<128>, gk, 3 * (4 * QT * 128 * 2 + QT * 8), stream, a);
   }
   OTAMD_CHECK_LAUNCH();
