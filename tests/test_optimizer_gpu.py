@@ -86,3 +86,36 @@ def test_state_dict_roundtrip(dev):
     opt.step()
     sched.step()
     assert abs(opt.param_groups[0]["lr"] - 2e-4) < 1e-12
+
+
+@pytest.mark.parametrize("sr,clip", [(True, False), (False, True)])
+def test_adamw_lut_matches_computed_path(dev, sr, clip, monkeypatch):
+    """The LDS denominator-table kernel (stores >= 4M elements) is bit-identical to the computed
+    path (oracle-pinned above) over every bf16 exp_avg_sq magnitude, -0.0 state and two groups."""
+    from onetrainer_amd import _lib, kernels as K
+    n = (1 << 22) + 4096
+    g0 = torch.Generator().manual_seed(7)
+    # grads over ~30 binades (incl. exact zeros), states spanning the bf16 range, -0.0 in v
+    g = (torch.randn(n, generator=g0) * torch.exp2(torch.randint(-30, 4, (n,), generator=g0).float()))
+    g[::97] = 0.0
+    m = torch.randn(n, generator=g0) * 1e-3
+    v = torch.exp2(torch.randint(-120, 10, (n,), generator=g0).float()) * torch.rand(n, generator=g0)
+    v[::89] = -0.0
+    v[::101] = 0.0
+    p = torch.randn(n, generator=g0) * 0.05
+    bufs = [t.to(torch.bfloat16).to(dev) for t in (p, g, m, v)]
+    split = n // 2 + 8 * 37
+    common = dict(one_minus_beta1=0.1, beta2=0.999, one_minus_beta2=1e-3, bc2_sqrt=0.0447, eps=1e-8, pad=0.0)
+    groups = [_lib.AdamwGroup(begin=0, end=split, wd_factor=1 - 1e-5, neg_step_size=-1e-3, **common),
+              _lib.AdamwGroup(begin=split, end=n, wd_factor=1.0, neg_step_size=-3e-4, **common)]
+    coef = torch.tensor([0.37], device=dev) if clip else None
+    outs = []
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("OTAMD_ADAMW_LUT", mode)
+        pp, gg, mm, vv = (t.clone() for t in bufs)
+        K.adamw_bf16(pp, gg, mm, vv, groups, clip_coef=coef, stochastic_rounding=sr, seed=99)
+        torch.cuda.synchronize()
+        outs.append([t.view(torch.int16).cpu() for t in (pp, mm, vv)])
+    for o in outs[1:]:
+        for a, b, name in zip(outs[0], o, "pmv"):
+            assert torch.equal(a, b), (name, int((a != b).sum()))

@@ -43,7 +43,7 @@ def family(name):
 
 def step_window(rows):
     ids = sorted(rows)
-    marks = [i for i in ids if "adamw_bf16_kernel" in rows[i][0]]
+    marks = [i for i in ids if "adamw_bf16" in rows[i][0]]
     if len(marks) >= 3:
         lo, hi = marks[-3], marks[-2]
     else:

@@ -17,7 +17,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("out")
-    ap.add_argument("--steps-kernel", default="adamw_bf16_kernel")
+    ap.add_argument("--steps-kernel", default="adamw_bf16")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)

@@ -12,7 +12,7 @@ import sqlite3
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--marker", default="adamw_bf16_kernel")
+    ap.add_argument("--marker", default="adamw_bf16")
     ap.add_argument("--top", type=int, default=12)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
