@@ -641,12 +641,20 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(const bf16_t* __restri
   const long long row = ((long long)blockIdx.x * 4 + w) * RPW + lane / L;
   if (row >= rows) return;
   const float mean = mean_in[row], rstd = rstd_in[row];
-  bf8 xr[CPL], dr[CPL];
+  // every HBM operand of the row is requested up front (x, dy and the residual gradient / previous dx
+  // to add): issuing the add-in loads after the row reductions exposed a second full memory latency
+  bf8 xr[CPL], dr[CPL], ar[CPL];
+  const bf16_t* add = res ? res : (accumulate ? dx : nullptr);
+  const long long ldadd = res ? ldres : lddx;
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int c8 = li + L * k;
     xr[k] = *reinterpret_cast<const bf8*>(x + row * ldx + c8 * 8);
     dr[k] = *reinterpret_cast<const bf8*>(dy + row * lddy + c8 * 8);
+  }
+  if (add) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) ar[k] = *reinterpret_cast<const bf8*>(add + row * ldadd + (li + L * k) * 8);
   }
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -671,14 +679,12 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(const bf16_t* __restri
     unpack8(xr[k], xf);
     unpack8(dr[k], dv);
     unpack8(*reinterpret_cast<const bf8*>(gamma + c8 * 8), gm);
-    float prev[8], rg[8];
-    if (accumulate) unpack8(*reinterpret_cast<const bf8*>(dx + row * lddx + c8 * 8), prev);
-    if (res) unpack8(*reinterpret_cast<const bf8*>(res + row * ldres + c8 * 8), rg);
+    float ad[8];
+    if (add) unpack8(ar[k], ad);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       o[j] = rstd * (dv[j] * gm[j] - m1 - (xf[j] - mean) * rstd * m2);
-      if (accumulate) o[j] += prev[j];
-      if (res) o[j] += rg[j];
+      if (add) o[j] += ad[j];
     }
     *reinterpret_cast<bf8*>(dx + row * lddx + c8 * 8) = pack8(o);
   }

@@ -66,6 +66,8 @@ def ln(R, C):
     dg = torch.empty(C, device=dev, dtype=BF)
     db = torch.empty(C, device=dev, dtype=BF)
     emit("layernorm_bwd", [R, C], timeit(lambda: K.layernorm_bwd(x, dy, g, st, dx=dx, dgamma=dg, dbeta=db)), 3 * e)
+    dres = torch.randn_like(x)
+    emit("layernorm_bwd_res(dx only)", [R, C], timeit(lambda: K.layernorm_bwd_res(x, dy, dres, g, st)), 4 * e)
 
 
 def geglu(R, F):
