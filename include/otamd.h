@@ -54,6 +54,7 @@ typedef struct GemmArgs {
      (z / bdiv) * s0 + (z % bdiv) * s1 elements ((image, head) pairs of [B, N, H*D] activations) */
   int batch, bdiv;
   long long sa0, sa1, sb0, sb1, sc0, sc1;
+  unsigned* tile_ctr;   /* set by the library (split-K fix-up counters); callers leave it NULL */
 } GemmArgs;
 
 typedef struct AttnArgs {

@@ -33,7 +33,8 @@ class GemmArgs(C.Structure):
                 ("A2", C.c_void_p), ("lda2", C.c_longlong), ("B2", C.c_void_p), ("ldb2", C.c_longlong),
                 ("K1", C.c_int), ("K2", C.c_int),
                 ("batch", C.c_int), ("bdiv", C.c_int), ("sa0", C.c_longlong), ("sa1", C.c_longlong),
-                ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong)]
+                ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong),
+                ("tile_ctr", C.c_void_p)]
 
 
 class AdamwGroup(C.Structure):

@@ -40,6 +40,10 @@ struct GemmArgs {
   // [B, N, H*D] activation are bdiv = H, s0 = batch stride, s1 = D.  batch <= 1: unbatched.
   int batch, bdiv;
   long long sa0, sa1, sb0, sb1, sc0, sc1;
+  // split-K arrival counters, one per output tile (set by the launcher, never by callers): the
+  // last workgroup of a tile to store its partial sums the slabs itself (no reduce launch);
+  // zero between launches (the last arriver resets its counter), per stream
+  unsigned* tile_ctr;
 };
 
 __device__ __forceinline__ void gemm_batch_offset(GemmArgs& a) {
@@ -66,12 +70,41 @@ __device__ __forceinline__ bool gemm_wide_ok(const GemmArgs& a) {
   return (al & 15) == 0 && (a.ldc % 8) == 0 && (!a.rowvec || (a.ldv % 8) == 0) && (!a.residual || (a.ldr % 8) == 0);
 }
 
+// Split-K slab access for the in-kernel fix-up: sc1 (device-coherent) buffer stores / loads go
+// past the XCD-private L2, so partials written by workgroups on other XCDs are visible to the
+// last arriver after an s_waitcnt + counter atomic -- no agent-scope fences (their L2
+// write-back + invalidate stalled every concurrently running kernel: step 150 -> 204 ms).
+// Offsets are byte offsets into the slab (< 2^31, checked by the launcher).
+typedef unsigned slab_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const GemmArgs& args) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)args.slab, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void slab_store_coh(const GemmArgs& args, long long e, float a, float b, float c, float d) {
+  slab_u4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, slab_rsrc(args), (int)(e * 4), 0, 16);
+}
+template <bool COH>
+__device__ __forceinline__ float4 slab_load(const GemmArgs& args, long long e) {
+  if constexpr (COH) {
+    const slab_u4 v = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(args), (int)(e * 4), 0, 16);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+  } else {
+    return *reinterpret_cast<const float4*>(args.slab + e);
+  }
+}
+
 // epilogue for 8 consecutive output columns n..n+7 of row m: same math as gemm_store4, 16-byte
 // loads / stores (half the store instructions of the 4-column form; the tail is issue-bound)
 __device__ __forceinline__ void gemm_store8(const GemmArgs& args, int m, int n, float (&v)[8], int split,
                                             bool use_slab) {
   if (use_slab) {
-    float* dst = args.slab + ((long long)split * args.M + m) * args.N + n;
+    const long long e = ((long long)split * args.M + m) * args.N + n;
+    if (args.tile_ctr) {
+      slab_store_coh(args, e, v[0], v[1], v[2], v[3]);
+      slab_store_coh(args, e + 4, v[4], v[5], v[6], v[7]);
+      return;
+    }
+    float* dst = args.slab + e;
     reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
     reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
     return;
@@ -105,8 +138,12 @@ __device__ __forceinline__ void gemm_store8(const GemmArgs& args, int m, int n, 
 __device__ __forceinline__ void gemm_store4(const GemmArgs& args, int m, int n, float (&v)[4], int split,
                                             bool use_slab) {
   if (use_slab) {
-    float* dst = args.slab + ((long long)split * args.M + m) * args.N + n;
-    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    const long long e = ((long long)split * args.M + m) * args.N + n;
+    if (args.tile_ctr) {
+      slab_store_coh(args, e, v[0], v[1], v[2], v[3]);
+      return;
+    }
+    *reinterpret_cast<float4*>(args.slab + e) = make_float4(v[0], v[1], v[2], v[3]);
     return;
   }
 #pragma unroll
@@ -167,3 +204,72 @@ __device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, in
 __device__ __forceinline__ int kimg_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 // MN-mode LDS image: [64 k rows][RB bytes], 32-byte block b of row k stored at b ^ s(k)
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+// alpha * sum_s slab[s] (+bias, +rowvec, +residual) (+C if accumulate) for V consecutive columns
+// n.. of row m: the split-K combine, shared by splitk_reduce_kernel and the GEMM's in-kernel
+// last-arriver fix-up so both give the same bits (splits summed in index order).
+template <int V, bool COH = false>
+__device__ __forceinline__ void splitk_combine(const GemmArgs& args, unsigned m, unsigned n, int splits) {
+  const long long MN = (long long)args.M * args.N;
+  const long long e = (long long)m * args.N + n;
+  float v[V];
+  {
+    const float4 t = slab_load<COH>(args, e);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    if constexpr (V == 8) {
+      const float4 u = slab_load<COH>(args, e + 4);
+      v[4] = u.x; v[5] = u.y; v[6] = u.z; v[7] = u.w;
+    }
+  }
+  int z = 1;
+  for (; z + 3 < splits; z += 4) {
+    float4 t[4][V / 4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int h = 0; h < V / 4; ++h) t[q][h] = slab_load<COH>(args, (z + q) * MN + e + 4 * h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int h = 0; h < V / 4; ++h) {
+        v[4 * h] += t[q][h].x; v[4 * h + 1] += t[q][h].y; v[4 * h + 2] += t[q][h].z; v[4 * h + 3] += t[q][h].w;
+      }
+  }
+  for (; z < splits; ++z)
+#pragma unroll
+    for (int h = 0; h < V / 4; ++h) {
+      const float4 t = slab_load<COH>(args, z * MN + e + 4 * h);
+      v[4 * h] += t.x; v[4 * h + 1] += t.y; v[4 * h + 2] += t.z; v[4 * h + 3] += t.w;
+    }
+#pragma unroll
+  for (int t = 0; t < V; ++t) v[t] *= args.alpha;
+  if (args.bias)
+#pragma unroll
+    for (int t = 0; t < V; ++t) v[t] += bf2f(args.bias[n + t]);
+  if (args.rowvec)
+#pragma unroll
+    for (int t = 0; t < V; ++t) v[t] += bf2f(args.rowvec[(long long)(m / args.rows_per_vec) * args.ldv + n + t]);
+  if (args.residual)
+#pragma unroll
+    for (int t = 0; t < V; ++t) v[t] += bf2f(args.residual[(long long)m * args.ldr + n + t]);
+  if (args.c_f32) {
+    float* dst = reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n;
+#pragma unroll
+    for (int t = 0; t < V; ++t) dst[t] = args.accumulate ? dst[t] + v[t] : v[t];
+  } else {
+    bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
+    if constexpr (V == 8) {
+      if (args.accumulate) {
+        float p[8];
+        unpack8(*reinterpret_cast<const bf8*>(dst), p);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += p[t];
+      }
+      *reinterpret_cast<bf8*>(dst) = pack8(v);
+    } else {
+#pragma unroll
+      for (int t = 0; t < V; ++t) dst[t] = f2bf(args.accumulate ? bf2f(dst[t]) + v[t] : v[t]);
+    }
+  }
+}
+

@@ -21,6 +21,9 @@
 #include "gemm.h"
 
 #include <stdlib.h>
+
+#include <mutex>
+#include <unordered_map>
 #include <string.h>
 
 #define BM 128
@@ -283,69 +286,9 @@ template <int V>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs args, int splits) {
   const unsigned NV = (unsigned)args.N / V;
   const unsigned total = (unsigned)args.M * NV;
-  const long long MN = (long long)args.M * args.N;
   for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     const unsigned m = i / NV, n = (i - m * NV) * V;
-    const long long e = (long long)m * args.N + n;
-    float v[V];
-    {
-      const float4 t = *reinterpret_cast<const float4*>(args.slab + e);
-      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-      if constexpr (V == 8) {
-        const float4 u = *reinterpret_cast<const float4*>(args.slab + e + 4);
-        v[4] = u.x; v[5] = u.y; v[6] = u.z; v[7] = u.w;
-      }
-    }
-    int z = 1;
-    for (; z + 3 < splits; z += 4) {
-      float4 t[4][V / 4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int h = 0; h < V / 4; ++h) t[q][h] = *reinterpret_cast<const float4*>(args.slab + (z + q) * MN + e + 4 * h);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int h = 0; h < V / 4; ++h) {
-          v[4 * h] += t[q][h].x; v[4 * h + 1] += t[q][h].y; v[4 * h + 2] += t[q][h].z; v[4 * h + 3] += t[q][h].w;
-        }
-    }
-    for (; z < splits; ++z)
-#pragma unroll
-      for (int h = 0; h < V / 4; ++h) {
-        const float4 t = *reinterpret_cast<const float4*>(args.slab + z * MN + e + 4 * h);
-        v[4 * h] += t.x; v[4 * h + 1] += t.y; v[4 * h + 2] += t.z; v[4 * h + 3] += t.w;
-      }
-#pragma unroll
-    for (int t = 0; t < V; ++t) v[t] *= args.alpha;
-    if (args.bias)
-#pragma unroll
-      for (int t = 0; t < V; ++t) v[t] += bf2f(args.bias[n + t]);
-    if (args.rowvec)
-#pragma unroll
-      for (int t = 0; t < V; ++t) v[t] += bf2f(args.rowvec[(long long)(m / args.rows_per_vec) * args.ldv + n + t]);
-    if (args.residual)
-#pragma unroll
-      for (int t = 0; t < V; ++t) v[t] += bf2f(args.residual[(long long)m * args.ldr + n + t]);
-    if (args.c_f32) {
-      float* dst = reinterpret_cast<float*>(args.C) + (long long)m * args.ldc + n;
-#pragma unroll
-      for (int t = 0; t < V; ++t) dst[t] = args.accumulate ? dst[t] + v[t] : v[t];
-    } else {
-      bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
-      if constexpr (V == 8) {
-        if (args.accumulate) {
-          float p[8];
-          unpack8(*reinterpret_cast<const bf8*>(dst), p);
-#pragma unroll
-          for (int t = 0; t < 8; ++t) v[t] += p[t];
-        }
-        *reinterpret_cast<bf8*>(dst) = pack8(v);
-      } else {
-#pragma unroll
-        for (int t = 0; t < V; ++t) dst[t] = f2bf(args.accumulate ? bf2f(dst[t]) + v[t] : v[t]);
-      }
-    }
+    splitk_combine<V>(args, m, n, splits);
   }
 }
 
@@ -483,6 +426,39 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
   return tile;
 }
 
+// Split-K arrival counters for the in-kernel fix-up (gemm2.hip), one array per stream: kernels
+// of one stream run in order and each last arriver re-zeroes its counter, so an array is all
+// zero whenever a launch starts.  Allocated (and zeroed) at the stream's first split-K launch.
+// OPT-IN (OTAMD_SPLITK_FIXUP=1): measured on the SDXL step it is slower than the reduce kernel
+// (150 -> 165 ms/step): each tile's last arriver sums 2-7 fp32 partials on ONE CU, a serial tail
+// per tile, while splitk_reduce_kernel spreads the same bytes over the whole chip.  Kept, with its
+// parity test, as the base for a fix-up spread over all split workgroups of a tile.
+#define SPLITK_MAX_TILES 65536
+static unsigned* splitk_counters(hipStream_t stream, long long tiles) {
+  if (tiles > SPLITK_MAX_TILES) return nullptr;
+  const char* e = getenv("OTAMD_SPLITK_FIXUP");
+  if (!e || e[0] != '1') return nullptr;
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, unsigned*> ctrs;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = ctrs.find(stream);
+  if (it != ctrs.end()) return it->second;
+  // no allocation while the stream is being captured into a graph: that launch keeps the reduce kernel
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  unsigned* p = nullptr;
+  if (hipMalloc(&p, SPLITK_MAX_TILES * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, SPLITK_MAX_TILES * sizeof(unsigned)) != hipSuccess) { (void)hipFree(p); return nullptr; }
+  ctrs.emplace(stream, p);
+  return p;
+}
+
+// workgroups along grid.x of a v2 launch (gemm2_launch's tile sizes)
+static long long tile_count(const GemmArgs& a, int tile) {
+  const int bm = (tile == 2 || tile == 4) ? 128 : 256, bn = (tile == 1 || tile == 4) ? 128 : 256;
+  return (long long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+}
+
 // force_tile: -9 = planned; otherwise the tile code (-1 v1, 0..3 v2) and splits >= 1 as given
 static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* workspace, long long ws_bytes,
                      hipStream_t stream) {
@@ -530,8 +506,15 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   int tile = force_tile == -9 ? resolve_tile(a, splits, plan, v2_only) : force_tile;
   if (v2_only && tile < 0) return OTAMD_EUNSUPPORTED;
   int rc = OTAMD_EUNSUPPORTED;
-  if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
+  a.tile_ctr = nullptr;
+  if (tile >= 0) {
+    if (splits > 1 && (long long)splits * a.M * a.N * 4 < (1LL << 31))   // sc1 slab offsets are 31-bit
+      a.tile_ctr = splitk_counters(stream, tile_count(a, tile));
+    rc = gemm2_launch(a, tile, splits, stream);
+  }
   if (rc == OTAMD_ELAUNCH) return rc;
+  const bool fixed_up = rc == OTAMD_OK && a.tile_ctr != nullptr;
+  a.tile_ctr = nullptr;
   if (rc != OTAMD_OK) {
     if (!fn || a.A2) return rc;   // v1 has no conv-weight B and no second K segment
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -539,7 +522,7 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);
     OTAMD_CHECK_LAUNCH();
   }
-  if (splits > 1) {
+  if (splits > 1 && !fixed_up) {
     // 8-wide needs 16-byte aligned rows of C (bf16: ldc % 8, fp32 handled element-wise)
     const bool v8 = (a.N % 8) == 0 && (a.ldc % 8) == 0 && ((uintptr_t)a.C & 15) == 0;
     const long long nv = (long long)a.M * a.N / (v8 ? 8 : 4);

@@ -358,6 +358,38 @@ __global__ void __launch_bounds__(NW * 64, (BM == 128 && BN == 128) ? 4 : NW / 4
         }
       }
     }
+    if (use_slab && args.tile_ctr) {
+      // Split-K fix-up: the last workgroup of this output tile to arrive sums every split's slab
+      // (index order, the reduce kernel's arithmetic) and writes C, so no reduce launch follows.
+      // The partials went out as sc1 stores; s_waitcnt vmcnt(0) has them at the coherence point
+      // before this workgroup's arrival is counted, and the last arriver reads them with sc1 loads.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // every wave's partial stored; LDS no longer read by the main loop
+      unsigned* flag = reinterpret_cast<unsigned*>(smem);
+      if (threadIdx.x == 0) {
+        unsigned* ctr = args.tile_ctr + blockIdx.x;
+        const unsigned last = atomicAdd(ctr, 1u) == gridDim.z - 1;
+        if (last) atomicExch(ctr, 0u);   // zero again for the stream's next split-K launch
+        flag[0] = last;
+      }
+      __syncthreads();
+      if (!flag[0]) return;
+      const int rows = min(BM, args.M - m0), cols = min(BN, args.N - n0);
+      const int splits = gridDim.z;
+      if ((args.N % 8) == 0 && (args.ldc % 8) == 0 && ((uintptr_t)args.C & 15) == 0) {
+        const int cu = cols / 8;
+        for (int u = threadIdx.x; u < rows * cu; u += NW * 64) {
+          const int r = u / cu;
+          splitk_combine<8, true>(args, (unsigned)(m0 + r), (unsigned)(n0 + 8 * (u - r * cu)), splits);
+        }
+      } else {
+        const int cu = cols / 4;
+        for (int u = threadIdx.x; u < rows * cu; u += NW * 64) {
+          const int r = u / cu;
+          splitk_combine<4, true>(args, (unsigned)(m0 + r), (unsigned)(n0 + 4 * (u - r * cu)), splits);
+        }
+      }
+    }
     return;
   }
 #pragma unroll
