@@ -123,6 +123,25 @@ def pmc_traffic():
         return json.load(f)
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a torchrun environment: start N fresh child ranks (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env) before this process touches the GPU, wait
+    for all of them and return the worst exit code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -141,6 +160,10 @@ def main():
                     help="time (tile, split-K) candidates per GEMM signature in warm-up instead of the analytic plan "
                          "(measured: no gain on the SDXL step -- isolated warm-cache timings do not transfer)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; n_gpus reports the world size")
 
     from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_sdxl_batch
     from onetrainer_amd.module.unet import flops_per_image, sd15_config, sdxl_config

@@ -283,9 +283,12 @@ int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s)
 /* replaces: ModelSetupNoiseMixin._create_noise (modules/modelSetup/mixin/ModelSetupNoiseMixin.py:18-49) */
 int otamd_noise(void* out, int f32, long long n, long long offset, unsigned long long seed, hipStream_t s);
 
-/* replaces: ModelSetupNoiseMixin._get_timestep_discrete (ModelSetupNoiseMixin.py:51-155) */
+/* replaces: ModelSetupNoiseMixin._get_timestep_discrete (ModelSetupNoiseMixin.py:51-155), UNIFORM (dist 0) and
+   LOGIT_NORMAL (dist 1) with static shift.  draws (nullable): injected per-sample draws instead of Philox --
+   the U[0,1) sample (UNIFORM) or the N(bias, weight+1) sample (LOGIT_NORMAL) of the reference's generator. */
 int otamd_timesteps(int* out, int n, long long sample0, unsigned long long seed, int dist, int
-    num_train_timesteps, float min_s, float max_s, float shift, float bias, float weight, hipStream_t s);
+    num_train_timesteps, float min_s, float max_s, float shift, float bias, float weight, const float* draws,
+    hipStream_t s);
 
 /* replaces: BaseStableDiffusionXLSetup.predict scale + _add_noise_discrete + get_velocity (BaseStableDiffusionXLSetup.py:214-236,277-291; ModelSetupDiffusionMixin.py:15-38) */
 int otamd_ddpm_prologue(const void* latent, const void* noise, int lat_f32, const int* timestep, const float*
@@ -297,10 +300,13 @@ int otamd_flow_prologue(const void* latent, const void* noise, int lat_f32, cons
     float shift_factor, int num_t, int B, long long HW, int C, int cpad, void* model_in, void* target,
     hipStream_t s);
 
-/* replaces: ModelSetupDiffusionLossMixin._diffusion_losses/__unmasked_losses + .mean() (ModelSetupDiffusionLossMixin.py:119-168,233-279; BaseStableDiffusionXLSetup.py:360-373) */
+/* replaces: ModelSetupDiffusionLossMixin._diffusion_losses / _flow_matching_losses / __unmasked_losses + .mean()
+   (ModelSetupDiffusionLossMixin.py:119-168,233-321; BaseStableDiffusionXLSetup.py:360-373; BaseFluxSetup.py:377-390).
+   loss_fn: 0 CONSTANT, 1 MIN_SNR_GAMMA, 2 DEBIASED_ESTIMATION, 3 P2 (sqrt_acp / sqrt_1m tables), 4 SIGMA
+   ((t+1)/num_t, flow matching).  B <= 1024. */
 int otamd_mse_loss(const void* pred, int cpad, const void* target, int tgt_f32, int B, long long HW, int C,
     float mse_strength, float scale, const float* loss_weight, const int* timestep, const float* sqrt_acp,
-    const float* sqrt_1m, int loss_fn, float gamma, int v_pred, float ga, float* ws, long long ws_floats,
+    const float* sqrt_1m, int loss_fn, float gamma, int v_pred, int num_t, float ga, float* ws, long long ws_floats,
     float* loss_out, float* coef, float* losses_out, hipStream_t s);
 
 /* replaces: autograd of the MSE loss */

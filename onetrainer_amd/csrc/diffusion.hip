@@ -65,25 +65,31 @@ __global__ void noise_kernel(void* out, int f32, long long n, long long offset, 
 }
 
 // timesteps for samples [sample0, sample0+n) of the global batch
-// dist 0 = UNIFORM, 1 = LOGIT_NORMAL (ModelSetupNoiseMixin.py:91-118)
+// dist 0 = UNIFORM, 1 = LOGIT_NORMAL (ModelSetupNoiseMixin.py:91-118).  draws != nullptr injects the
+// random draw of each sample instead of Philox (parity tests): UNIFORM -> the U[0,1) sample of
+// torch.rand, LOGIT_NORMAL -> the N(bias, weight + 1) sample of torch.normal (bias / weight unused).
 __global__ void timestep_kernel(int* out, int n, long long sample0, unsigned long long seed, int dist,
                                 int num_train_timesteps, float min_s, float max_s, float shift, float bias,
-                                float weight) {
+                                float weight, const float* draws) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int mn = (int)(num_train_timesteps * min_s), mx = (int)(num_train_timesteps * max_s);
+  // int(num_train_timesteps * strength): the python product is a double, truncated toward zero
+  const int mn = (int)((double)num_train_timesteps * (double)min_s), mx = (int)((double)num_train_timesteps * (double)max_s);
   float t;
   if (dist == 0) {
-    const float u = philox_uniform(seed, 2u, (uint64_t)(sample0 + i));
+    const float u = draws ? draws[i] : philox_uniform(seed, 2u, (uint64_t)(sample0 + i));
     t = (float)mn + (float)(mx - mn) * u;
   } else {
-    const float z = philox_normal(seed, 3u, (uint64_t)(sample0 + i));
-    const float nrm = bias + (weight + 1.f) * z;
+    const float nrm = draws ? draws[i] : bias + (weight + 1.f) * philox_normal(seed, 3u, (uint64_t)(sample0 + i));
     const float lg = 1.f / (1.f + expf(-nrm));
     t = lg * (float)(mx - mn) + (float)mn;
   }
+  // num_train_timesteps * shift * t / ((shift - 1) * t + num_train_timesteps): python scalars enter the
+  // fp32 tensor ops as fp32 (N * shift is a python product, rounded once)
   const float N = (float)num_train_timesteps;
-  t = (N * shift * t) / ((shift - 1.f) * t + N);
+  const float Ns = (float)((double)num_train_timesteps * (double)shift);
+  const float sm1 = (float)((double)shift - 1.0);
+  t = (Ns * t) / (sm1 * t + N);
   out[i] = (int)t;   // .int() truncation
 }
 
@@ -166,21 +172,24 @@ __global__ void __launch_bounds__(256) mse_partial_kernel(const bf16_t* pred, in
   if (threadIdx.x == 0) partial[b * nblk + blk] = s;
 }
 
-// MSE pass 2 (1 block): losses[b] = mean * mse_strength * scale * loss_weight[b] * snr_w[b];
+// MSE pass 2 (1 block): losses[b] = mean * mse_strength * scale * loss_weight[b] * w_t[b];
 // loss = mean_b(losses) / ga ; coef[b] = d loss / d pred (without the 2*(p-t) factor)
-// loss_fn: 0 constant, 1 min-snr-gamma, 2 debiased estimation, 3 p2 (ModelSetupDiffusionLossMixin.py:170-231)
+// loss_fn: 0 constant, 1 min-snr-gamma, 2 debiased estimation, 3 p2 (ModelSetupDiffusionLossMixin.py:170-225),
+// 4 sigma = (t + 1) / num_t (flow matching, :226-231,297-300,317-319).  The per-sample losses are
+// summed in sample order by one lane (deterministic, like the reference's .mean()).
+#define LOSS_MAX_B 1024
 __global__ void mse_finalize_kernel(const float* partial, int nblk, int B, long long per, float mse_strength,
                                     float scale, const float* loss_weight, const int* timestep, const float* sqrt_acp,
-                                    const float* sqrt_1m, int loss_fn, float gamma, int v_pred, float ga,
+                                    const float* sqrt_1m, int loss_fn, float gamma, int v_pred, int num_t, float ga,
                                     float* loss_out, float* coef, float* losses_out) {
-  __shared__ float lsum[1];
-  if (threadIdx.x == 0) lsum[0] = 0.f;
-  __syncthreads();
+  __shared__ float lb_s[LOSS_MAX_B];
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     float s = 0.f;
     for (int k = 0; k < nblk; ++k) s += partial[b * nblk + k];
     float w = mse_strength * scale * (loss_weight ? loss_weight[b] : 1.f);
-    if (loss_fn != 0) {
+    if (loss_fn == 4) {
+      w *= (float)(timestep[b] + 1) / (float)num_t;
+    } else if (loss_fn != 0) {
       const int t = timestep[b];
       const float r = sqrt_acp[t] / sqrt_1m[t];
       float snr = r * r;
@@ -200,11 +209,15 @@ __global__ void mse_finalize_kernel(const float* partial, int nblk, int B, long 
     const float mean = s / (float)per;
     const float lb = mean * w;
     if (losses_out) losses_out[b] = lb;
-    atomicAdd(&lsum[0], lb);
+    lb_s[b] = lb;
     coef[b] = 2.f * w / ((float)per * (float)B * ga);
   }
   __syncthreads();
-  if (threadIdx.x == 0) loss_out[0] = lsum[0] / (float)B / ga;
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int b = 0; b < B; ++b) tot += lb_s[b];
+    loss_out[0] = tot / (float)B / ga;
+  }
 }
 
 // dpred = 2 (pred - target) * coef[b] * grad_out[0]; padded channels get 0
@@ -239,10 +252,10 @@ OTAMD_API int otamd_noise(void* out, int f32, long long n, long long offset, uns
 }
 OTAMD_API int otamd_timesteps(int* out, int n, long long sample0, unsigned long long seed, int dist,
                               int num_train_timesteps, float min_s, float max_s, float shift, float bias, float weight,
-                              hipStream_t s) {
+                              const float* draws, hipStream_t s) {
   if (!out || n <= 0 || num_train_timesteps <= 0 || (dist != 0 && dist != 1)) return OTAMD_EINVAL;
   timestep_kernel<<<(n + 63) / 64, 64, 0, s>>>(out, n, sample0, seed, dist, num_train_timesteps, min_s, max_s, shift,
-                                               bias, weight);
+                                               bias, weight, draws);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
@@ -272,17 +285,20 @@ OTAMD_API int otamd_flow_prologue(const void* latent, const void* noise, int lat
 OTAMD_API int otamd_mse_loss(const void* pred, int cpad, const void* target, int tgt_f32, int B, long long HW, int C,
                              float mse_strength, float scale, const float* loss_weight, const int* timestep,
                              const float* sqrt_acp, const float* sqrt_1m, int loss_fn, float gamma, int v_pred,
-                             float ga, float* ws, long long ws_floats, float* loss_out, float* coef, float* losses_out,
-                             hipStream_t s) {
-  if (!pred || !target || !ws || !loss_out || !coef || B <= 0 || C <= 0 || cpad < C) return OTAMD_EINVAL;
-  if (loss_fn != 0 && (!timestep || !sqrt_acp || !sqrt_1m)) return OTAMD_EINVAL;
+                             int num_t, float ga, float* ws, long long ws_floats, float* loss_out, float* coef,
+                             float* losses_out, hipStream_t s) {
+  if (!pred || !target || !ws || !loss_out || !coef || B <= 0 || B > LOSS_MAX_B || C <= 0 || cpad < C ||
+      loss_fn < 0 || loss_fn > 4)
+    return OTAMD_EINVAL;
+  if (loss_fn == 4 && (!timestep || num_t <= 0)) return OTAMD_EINVAL;
+  if (loss_fn != 0 && loss_fn != 4 && (!timestep || !sqrt_acp || !sqrt_1m)) return OTAMD_EINVAL;
   const long long per = HW * C;
   const int nblk = (int)((per + LOSS_BLK - 1) / LOSS_BLK);
   if (ws_floats < (long long)B * nblk) return OTAMD_EINVAL;
   mse_partial_kernel<<<dim3(nblk, B), 256, 0, s>>>((const bf16_t*)pred, cpad, target, tgt_f32, HW, C, ws, nblk);
   OTAMD_CHECK_LAUNCH();
   mse_finalize_kernel<<<1, 256, 0, s>>>(ws, nblk, B, per, mse_strength, scale, loss_weight, timestep, sqrt_acp, sqrt_1m,
-                                        loss_fn, gamma, v_pred, ga, loss_out, coef, losses_out);
+                                        loss_fn, gamma, v_pred, num_t, ga, loss_out, coef, losses_out);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

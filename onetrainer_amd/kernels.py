@@ -838,13 +838,17 @@ def noise(shape, seed, offset=0, dtype=BF16, device=None, out=None):
 
 
 def timesteps(n, seed, sample0=0, dist=0, num_train_timesteps=1000, min_s=0.0, max_s=1.0, shift=1.0, bias=0.0,
-              weight=0.0, device=None, out=None):
+              weight=0.0, device=None, out=None, draws=None):
+    """draws: optional f32 [n] injected draws (U[0,1) for UNIFORM, the N(bias, weight+1) sample for LOGIT_NORMAL)."""
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=device)
     _req(out.numel() == n and out.dtype == torch.int32 and out.is_contiguous(), "timesteps out")
+    if draws is not None:
+        _req(draws.dtype == F32 and draws.numel() == n and draws.is_contiguous() and draws.device == out.device,
+             "timestep draws: f32 [n] on the output's device")
     check(lib().otamd_timesteps(_p(out), n, sample0, seed & 0xFFFFFFFFFFFFFFFF, dist, num_train_timesteps,
-                                float(min_s), float(max_s), float(shift), float(bias), float(weight), stream_handle()),
-          "otamd_timesteps")
+                                float(min_s), float(max_s), float(shift), float(bias), float(weight), _p(draws),
+                                stream_handle()), "otamd_timesteps")
     return out
 
 
@@ -875,11 +879,11 @@ def flow_prologue(latent, noise_, timestep, scaling_factor, shift_factor, num_t=
     return model_in, target
 
 
-LOSS_FN = {"CONSTANT": 0, "MIN_SNR_GAMMA": 1, "DEBIASED_ESTIMATION": 2, "P2": 3}
+LOSS_FN = {"CONSTANT": 0, "MIN_SNR_GAMMA": 1, "DEBIASED_ESTIMATION": 2, "P2": 3, "SIGMA": 4}
 
 
 def mse_loss(pred, target, loss_weight=None, mse_strength=1.0, scale=1.0, loss_fn=0, gamma=5.0, v_pred=False,
-             ga=1.0, timestep=None, coeffs=None):
+             ga=1.0, timestep=None, coeffs=None, num_t=1000):
     """pred NHWC bf16 [B,H,W,cpad] (first C channels used), target [B,H,W,C] -> (loss f32[1], coef f32[B], losses)."""
     B, H, W, cpad = pred.shape
     C_ = target.shape[-1]
@@ -893,8 +897,8 @@ def mse_loss(pred, target, loss_weight=None, mse_strength=1.0, scale=1.0, loss_f
     acp, sq, s1m = coeffs if coeffs is not None else (None, None, None)
     check(lib().otamd_mse_loss(_p(pred), cpad, _p(target), int(target.dtype == F32), B, H * W, C_, float(mse_strength),
                                float(scale), _p(loss_weight), _p(timestep), _p(sq), _p(s1m), int(loss_fn),
-                               float(gamma), int(v_pred), float(ga), _p(ws), B * nblk, _p(loss), _p(coef),
-                               _p(losses), stream_handle()), "otamd_mse_loss")
+                               float(gamma), int(v_pred), int(num_t), float(ga), _p(ws), B * nblk, _p(loss),
+                               _p(coef), _p(losses), stream_handle()), "otamd_mse_loss")
     return loss, coef, losses
 
 

@@ -20,6 +20,8 @@ import torch
 from .. import kernels as K
 from ..module import flux_ops as O
 from ..module import functional as Fn
+from .BaseStableDiffusionXLSetup import loss_plan, nhwc_pair, timestep_plan
+from ..util.config.plain import plain
 
 
 class BaseFluxSetup:
@@ -38,6 +40,7 @@ class BaseFluxSetup:
 
     def _text(self, batch, config, rand, B):
         """FluxModel.encode_text with cached outputs: per-encoder dropout masks from Random(seed)."""
+        config = plain(config)
         pooled = batch["text_encoder_1_pooled_state"]
         ehs = batch["text_encoder_2_hidden_state"]
         p1, p2 = config.text_encoder.dropout_probability, config.text_encoder_2.dropout_probability
@@ -52,6 +55,7 @@ class BaseFluxSetup:
     def _shift(self, config, h, w):
         """ModelSetupNoiseMixin._get_timestep_discrete: static timestep_shift, or the dynamic one of the
         image sequence length (base 256 -> 0.5, max 4096 -> 1.15, patch 2)."""
+        config = plain(config)
         if not config.dynamic_timestep_shifting:
             return config.timestep_shift
         m = (1.15 - 0.5) / (4096 - 256)
@@ -59,6 +63,7 @@ class BaseFluxSetup:
         return math.exp(mu)
 
     def predict(self, model, batch: dict, config, train_progress, *, deterministic: bool = False) -> dict:
+        config = plain(config)
         if config.offset_noise_weight > 0 or config.perturbation_noise_weight > 0:
             raise NotImplementedError("offset / perturbation noise are not on this build's hot path yet")
         batch_seed = 0 if deterministic else train_progress.global_step
@@ -73,8 +78,7 @@ class BaseFluxSetup:
         if deterministic:
             timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=latent.device)
         else:
-            dist = {"UNIFORM": 0, "LOGIT_NORMAL": 1}[config.timestep_distribution]
-            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=dist, num_train_timesteps=N,
+            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=timestep_plan(config), num_train_timesteps=N,
                                    min_s=config.min_noising_strength, max_s=config.max_noising_strength,
                                    shift=self._shift(config, h, w), bias=config.noising_bias,
                                    weight=config.noising_weight, device=latent.device)
@@ -87,17 +91,17 @@ class BaseFluxSetup:
             guidance = torch.full((B,), float(config.prior.guidance_scale), dtype=torch.float32, device=latent.device)
         pred_tok = model.transformer(tokens, timestep.float() / 1000, guidance, pooled, ehs, h, w)
         pred = O.UnpackFn.apply(pred_tok, B, h, w, C)
-        return {"loss_type": "target", "timestep": timestep, "predicted": pred, "target": target}
+        # reference contract: [B, 16, h, w] (BaseFluxSetup.py:301-307); views of the NHWC kernel tensors
+        return {"loss_type": "target", "timestep": timestep, "predicted": pred.permute(0, 3, 1, 2),
+                "target": target.permute(0, 3, 1, 2), "_predicted_nhwc": pred, "_target_nhwc": target}
 
     def calculate_loss(self, model, batch: dict, data: dict, config) -> torch.Tensor:
         """_flow_matching_losses(...).mean() (BaseFluxSetup.py:377-390): unmasked MSE x loss_weight x scalers."""
-        if config.mae_strength != 0 or config.log_cosh_strength != 0 or config.masked_training:
-            raise NotImplementedError("only the unmasked MSE loss of C1-C5 is on this build's hot path")
-        if config.loss_weight_fn != "CONSTANT":
-            raise NotImplementedError(f"flow-matching loss weight {config.loss_weight_fn}")
-        bs = 1 if config.loss_scaler in ("NONE", "GRADIENT_ACCUMULATION") else config.batch_size
-        gas = 1 if config.loss_scaler in ("NONE", "BATCH") else config.gradient_accumulation_steps
+        plan = loss_plan(plain(config), flow=True)
         lw = batch.get("loss_weight")
         lw = lw.to(self.train_device, torch.float32).contiguous() if lw is not None else None
-        return Fn.MSELossFn.apply(data["predicted"], data["target"], lw, data["timestep"], None, 0, 5.0, False, 1.0,
-                                  config.mse_strength, float(bs * gas), 1.0 / self.dp_world)
+        pred, target = nhwc_pair(data, 16)
+        N = model.noise_scheduler.config["num_train_timesteps"]
+        return Fn.MSELossFn.apply(pred, target, lw, data["timestep"], None, plan["loss_fn"], plan["gamma"], False, 1.0,
+                                  plan["mse_strength"], float(plan["batch_size_scale"] * plan["ga_scale"]),
+                                  1.0 / self.dp_world, N)

@@ -13,12 +13,14 @@ from __future__ import annotations
 import torch
 
 from .BaseStableDiffusionXLSetup import BaseStableDiffusionXLSetup
+from ..util.config.plain import plain
 
 
 class BaseStableDiffusionSetup(BaseStableDiffusionXLSetup):
     def _text(self, model, batch, config, rand, B):
         """StableDiffusionModel.encode_text with cached text (StableDiffusionModel.py:188-233):
         pass-through, then the per-sample dropout mask drawn from Random(batch_seed)."""
+        config = plain(config)
         te = batch["text_encoder_hidden_state"]
         p = config.text_encoder.dropout_probability
         if p is not None and p > 0:

@@ -18,8 +18,56 @@ import torch
 
 from .. import kernels as K
 from ..module import functional as Fn
+from ..util.config.plain import plain
 
 LOSS_FN = {"CONSTANT": 0, "MIN_SNR_GAMMA": 1, "DEBIASED_ESTIMATION": 2, "P2": 3}
+TIMESTEP_DIST = {"UNIFORM": 0, "LOGIT_NORMAL": 1}
+
+
+def loss_plan(config, flow: bool = False) -> dict:
+    """The loss decisions of ModelSetupDiffusionLossMixin for this config (config already plain()):
+    batch / GA scale (LossScaler, :243-248 / :290-295) and the timestep weight kernel id (:271-278 for
+    DDPM: MIN_SNR_GAMMA / DEBIASED_ESTIMATION / P2, anything else unweighted; :316-319 for flow
+    matching: SIGMA, anything else unweighted)."""
+    if config.mae_strength != 0 or config.log_cosh_strength != 0 or config.masked_training:
+        raise NotImplementedError("only the unmasked MSE loss of C1-C5 is on this build's hot path")
+    scaler = config.loss_scaler
+    if scaler not in ("NONE", "BATCH", "GRADIENT_ACCUMULATION", "BOTH"):
+        raise ValueError(f"loss_scaler {scaler!r}")
+    bs = 1 if scaler in ("NONE", "GRADIENT_ACCUMULATION") else config.batch_size
+    gas = 1 if scaler in ("NONE", "BATCH") else config.gradient_accumulation_steps
+    fn = config.loss_weight_fn
+    if flow:
+        kid = 4 if fn == "SIGMA" else 0
+    else:
+        kid = LOSS_FN.get(fn, 0)
+    return {"batch_size_scale": bs, "ga_scale": gas, "loss_fn": kid, "gamma": float(config.loss_weight_strength),
+            "mse_strength": float(config.mse_strength)}
+
+
+def timestep_plan(config) -> int:
+    """kernel id of config.timestep_distribution (ModelSetupNoiseMixin.py:91-118); the discrete
+    SIGMOID / COS_MAP / HEAVY_TAIL samplers are outside C1-C5."""
+    d = config.timestep_distribution
+    if d not in TIMESTEP_DIST:
+        raise NotImplementedError(f"timestep distribution {d} is not on this build's hot path")
+    return TIMESTEP_DIST[d]
+
+
+def nhwc_pair(data: dict, C: int):
+    """(pred NHWC bf16 [B,h,w,cpad], target NHWC [B,h,w,C]) for the loss kernel: the private kernel
+    tensors predict() returned, or -- when a caller hands [B,C,h,w] tensors of its own -- their
+    NHWC restatement (pred padded to 8 channels, the kernel's 16-byte row granule)."""
+    if "_predicted_nhwc" in data:
+        return data["_predicted_nhwc"], data["_target_nhwc"]
+    p, t = data["predicted"], data["target"]
+    if p.dim() == 4 and p.shape[1] == C and p.shape[-1] != C:
+        p = p.permute(0, 2, 3, 1)
+        t = t.permute(0, 2, 3, 1)
+    cpad = (p.shape[-1] + 7) // 8 * 8
+    if cpad != p.shape[-1]:
+        p = torch.nn.functional.pad(p, (0, cpad - p.shape[-1]))
+    return p.to(torch.bfloat16).contiguous(), t.contiguous()
 
 
 class BaseStableDiffusionXLSetup:
@@ -39,6 +87,7 @@ class BaseStableDiffusionXLSetup:
         return lat.contiguous()
 
     def _text(self, model, batch, config, rand, B):
+        config = plain(config)
         te1 = batch["text_encoder_1_hidden_state"]
         te2 = batch.get("text_encoder_2_hidden_state")
         pooled = batch.get("text_encoder_2_pooled_state")
@@ -58,6 +107,7 @@ class BaseStableDiffusionXLSetup:
     def graphable(self, config) -> bool:
         """the step has no host-random or host-varying input besides (noise, timestep), so it can be
         captured once and replayed (text dropout draws its mask on the host per step)."""
+        config = plain(config)
         parts = [config.text_encoder] + ([config.text_encoder_2] if hasattr(config, "text_encoder_2") else [])
         return (config.offset_noise_weight <= 0 and config.perturbation_noise_weight <= 0
                 and all(not (p.dropout_probability or 0) > 0 for p in parts))
@@ -65,6 +115,7 @@ class BaseStableDiffusionXLSetup:
     def step_inputs(self, model, batch: dict, config, train_progress, *, deterministic: bool = False, out=None):
         """(noise, timestep) of this micro-step (ModelSetupNoiseMixin._create_noise /
         _get_timestep_discrete): Philox seeded by `batch_seed`, counter = GLOBAL batch index."""
+        config = plain(config)
         batch_seed = 0 if deterministic else train_progress.global_step
         lat = batch["latent_image"]
         B = lat.shape[0]
@@ -79,8 +130,7 @@ class BaseStableDiffusionXLSetup:
             if out is not None:
                 timestep = out[1].copy_(timestep)
         else:
-            dist = {"UNIFORM": 0, "LOGIT_NORMAL": 1}[config.timestep_distribution]
-            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=dist, num_train_timesteps=N,
+            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=timestep_plan(config), num_train_timesteps=N,
                                    min_s=config.min_noising_strength, max_s=config.max_noising_strength,
                                    shift=config.timestep_shift, bias=config.noising_bias,
                                    weight=config.noising_weight, device=lat.device,
@@ -88,6 +138,7 @@ class BaseStableDiffusionXLSetup:
         return noise, timestep
 
     def predict(self, model, batch: dict, config, train_progress, *, deterministic: bool = False) -> dict:
+        config = plain(config)
         if config.offset_noise_weight > 0 or config.perturbation_noise_weight > 0:
             raise NotImplementedError("offset / perturbation noise are not on this build's hot path yet")
         batch_seed = 0 if deterministic else train_progress.global_step
@@ -110,17 +161,19 @@ class BaseStableDiffusionXLSetup:
                                     batch["crop_resolution"][0], batch["crop_resolution"][1]], dim=1).to(
                 latent.device, torch.float32)
         pred = model.unet(unet_in, timestep, ehs, pooled, time_ids)
-        return {"loss_type": "target", "timestep": timestep, "predicted": pred, "target": target,
-                "prediction_type": ptype}
+        # the reference contract: predicted / target are [B, 4, h, w] (BaseStableDiffusionXLSetup.py:277-291);
+        # here they are views of the NHWC kernel tensors (pred carries 4 zero pad channels), which
+        # calculate_loss reads directly through the private keys
+        return {"loss_type": "target", "timestep": timestep,
+                "predicted": pred[..., :C].permute(0, 3, 1, 2), "target": target.permute(0, 3, 1, 2),
+                "prediction_type": ptype, "_predicted_nhwc": pred, "_target_nhwc": target}
 
     def calculate_loss(self, model, batch: dict, data: dict, config) -> torch.Tensor:
-        if config.mae_strength != 0 or config.log_cosh_strength != 0 or config.masked_training:
-            raise NotImplementedError("only the unmasked MSE loss of C1-C5 is on this build's hot path")
-        bs = 1 if config.loss_scaler in ("NONE", "GRADIENT_ACCUMULATION") else config.batch_size
-        gas = 1 if config.loss_scaler in ("NONE", "BATCH") else config.gradient_accumulation_steps
+        plan = loss_plan(plain(config))
         lw = batch.get("loss_weight")
         lw = lw.to(self.train_device, torch.float32).contiguous() if lw is not None else None
-        return Fn.MSELossFn.apply(data["predicted"], data["target"], lw, data["timestep"],
-                                  model.noise_scheduler.coeffs, LOSS_FN[config.loss_weight_fn],
-                                  config.loss_weight_strength, data.get("prediction_type") == "v_prediction", 1.0,
-                                  config.mse_strength, float(bs * gas), 1.0 / self.dp_world)
+        pred, target = nhwc_pair(data, 4)
+        return Fn.MSELossFn.apply(pred, target, lw, data["timestep"], model.noise_scheduler.coeffs, plan["loss_fn"],
+                                  plan["gamma"], data.get("prediction_type") == "v_prediction", 1.0,
+                                  plan["mse_strength"], float(plan["batch_size_scale"] * plan["ga_scale"]),
+                                  1.0 / self.dp_world)

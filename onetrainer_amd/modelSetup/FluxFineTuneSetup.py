@@ -8,10 +8,12 @@ from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupC
 from ..util.optimizer.adamw_fused import FusedAdamW
 from ..util.optimizer_util import restore_training_state
 from .BaseFluxSetup import BaseFluxSetup
+from ..util.config.plain import plain
 
 
 class FluxFineTuneSetup(BaseFluxSetup):
     def create_parameters(self, model, config) -> NamedParameterGroupCollection:
+        config = plain(config)
         pgc = NamedParameterGroupCollection()
         if config.text_encoder.train or config.text_encoder_2.train:
             raise NotImplementedError("text-encoder training is outside this build's hot path (text is cached)")
@@ -21,9 +23,11 @@ class FluxFineTuneSetup(BaseFluxSetup):
         return pgc
 
     def setup_optimizations(self, model, config):
+        config = plain(config)
         model.train_dtype = torch.bfloat16
 
     def setup_model(self, model, config):
+        config = plain(config)
         self.setup_optimizations(model, config)
         params = self.create_parameters(model, config)
         model.parameters = params
@@ -41,10 +45,13 @@ class FluxFineTuneSetup(BaseFluxSetup):
         restore_training_state(model, config)
 
     def setup_train_device(self, model, config):
+        config = plain(config)
         pass
 
     def after_optimizer_step(self, model, config, train_progress):
+        config = plain(config)
         pass
 
     def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
+        config = plain(config)
         pass

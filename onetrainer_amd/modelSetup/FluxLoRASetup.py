@@ -11,6 +11,7 @@ from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupC
 from ..util.optimizer.adamw_fused import FusedAdamW
 from ..util.optimizer_util import restore_training_state
 from .BaseFluxSetup import BaseFluxSetup
+from ..util.config.plain import plain
 
 PRESETS = {"attn-mlp": ["attn", "ff.net"], "attn-only": ["attn"], "full": []}
 
@@ -18,11 +19,13 @@ PRESETS = {"attn-mlp": ["attn", "ff.net"], "attn-only": ["attn"], "full": []}
 class FluxLoRASetup(BaseFluxSetup):
     @staticmethod
     def layer_filter(config):
+        config = plain(config)
         if config.lora_layers:
             return config.lora_layers.split(",")
         return PRESETS.get(config.lora_layer_preset or "full", [])
 
     def create_parameters(self, model, config) -> NamedParameterGroupCollection:
+        config = plain(config)
         pgc = NamedParameterGroupCollection()
         if config.text_encoder.train or config.text_encoder_2.train:
             raise NotImplementedError("text-encoder LoRA is outside this build's hot path (text is cached)")
@@ -32,9 +35,11 @@ class FluxLoRASetup(BaseFluxSetup):
         return pgc
 
     def setup_optimizations(self, model, config):
+        config = plain(config)
         model.train_dtype = torch.bfloat16
 
     def setup_model(self, model, config):
+        config = plain(config)
         if getattr(config, "lora_decompose", False) or config.peft_type != "LORA":
             raise NotImplementedError("DoRA / LoHa are not on this build's hot path")
         if config.dropout_probability and config.dropout_probability > 0:
@@ -66,10 +71,13 @@ class FluxLoRASetup(BaseFluxSetup):
         restore_training_state(model, config)
 
     def setup_train_device(self, model, config):
+        config = plain(config)
         pass
 
     def after_optimizer_step(self, model, config, train_progress):
+        config = plain(config)
         model.transformer_lora.refresh()
 
     def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
+        config = plain(config)
         pass

@@ -8,10 +8,12 @@ from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupC
 from ..util.optimizer.adamw_fused import FusedAdamW
 from ..util.optimizer_util import restore_training_state
 from .BaseStableDiffusionXLSetup import BaseStableDiffusionXLSetup
+from ..util.config.plain import plain
 
 
 class StableDiffusionXLFineTuneSetup(BaseStableDiffusionXLSetup):
     def create_parameters(self, model, config) -> NamedParameterGroupCollection:
+        config = plain(config)
         pgc = NamedParameterGroupCollection()
         if config.unet.train:
             pgc.add_group(NamedParameterGroup("unet", model.unet.parameters(), config.unet.learning_rate))
@@ -22,9 +24,11 @@ class StableDiffusionXLFineTuneSetup(BaseStableDiffusionXLSetup):
     def setup_optimizations(self, model, config):
         # no gradient checkpointing: 288 GB HBM holds every activation;
         # no autocast: the kernels fix the compute dtype (bf16 GEMMs, fp32 norms/softmax/loss)
+        config = plain(config)
         model.train_dtype = torch.bfloat16
 
     def setup_model(self, model, config):
+        config = plain(config)
         self.setup_optimizations(model, config)
         params = self.create_parameters(model, config)
         model.parameters = params
@@ -42,10 +46,13 @@ class StableDiffusionXLFineTuneSetup(BaseStableDiffusionXLSetup):
         restore_training_state(model, config)
 
     def setup_train_device(self, model, config):
+        config = plain(config)
         pass   # model and data are created on the train device
 
     def after_optimizer_step(self, model, config, train_progress):
+        config = plain(config)
         pass
 
     def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
+        config = plain(config)
         pass

@@ -12,10 +12,12 @@ from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupC
 from ..util.optimizer.adamw_fused import FusedAdamW
 from ..util.optimizer_util import restore_training_state
 from .BaseStableDiffusionXLSetup import BaseStableDiffusionXLSetup
+from ..util.config.plain import plain
 
 
 class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
     def create_parameters(self, model, config) -> NamedParameterGroupCollection:
+        config = plain(config)
         pgc = NamedParameterGroupCollection()
         if config.text_encoder.train or config.text_encoder_2.train:
             raise NotImplementedError("text-encoder LoRA is outside this build's hot path (text is cached)")
@@ -25,15 +27,18 @@ class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
         return pgc
 
     def setup_optimizations(self, model, config):
+        config = plain(config)
         model.train_dtype = torch.bfloat16
 
     @staticmethod
     def layer_filter(config):
+        config = plain(config)
         if config.lora_layers:
             return config.lora_layers.split(",")
         return PRESETS.get(config.lora_layer_preset or "full", [])
 
     def setup_model(self, model, config):
+        config = plain(config)
         if getattr(config, "lora_decompose", False) or config.peft_type != "LORA":
             raise NotImplementedError("DoRA / LoHa are not on this build's hot path")
         if config.dropout_probability and config.dropout_probability > 0:
@@ -64,10 +69,13 @@ class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
         restore_training_state(model, config)
 
     def setup_train_device(self, model, config):
+        config = plain(config)
         pass
 
     def after_optimizer_step(self, model, config, train_progress):
+        config = plain(config)
         model.unet_lora.refresh()
 
     def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
+        config = plain(config)
         pass

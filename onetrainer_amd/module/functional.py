@@ -448,10 +448,10 @@ class MSELossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pred, target, loss_weight, timestep, coeffs, loss_fn, gamma, v_pred, ga, mse_strength, scale,
-                grad_scale=1.0):
+                grad_scale=1.0, num_t=1000):
         loss, coef, losses = K.mse_loss(pred, target, loss_weight, mse_strength=mse_strength, scale=scale,
                                         loss_fn=loss_fn, gamma=gamma, v_pred=v_pred, ga=ga, timestep=timestep,
-                                        coeffs=coeffs)
+                                        coeffs=coeffs, num_t=num_t)
         ctx.save_for_backward(pred, target, coef)
         ctx.losses = losses
         ctx.grad_scale = grad_scale
@@ -463,4 +463,4 @@ class MSELossFn(torch.autograd.Function):
         gd = g.reshape(1).float()
         if ctx.grad_scale != 1.0:   # data-parallel: fold 1/world into the loss gradient (sum all-reduce = mean)
             gd = gd * ctx.grad_scale
-        return (K.mse_grad(pred, target, coef, grad_out=gd.contiguous()),) + (None,) * 11
+        return (K.mse_grad(pred, target, coef, grad_out=gd.contiguous()),) + (None,) * 12

@@ -20,6 +20,7 @@ import time
 import torch
 
 from ..util import create
+from ..util.config.plain import plain
 from ..util.lr_scheduler_util import create_lr_scheduler
 from ..util.TrainProgress import TrainProgress
 from .ddp import GradBucketReducer, init_from_env
@@ -28,7 +29,7 @@ from .ddp import GradBucketReducer, init_from_env
 class GenericTrainer:
     def __init__(self, config, callbacks=None, commands=None, model=None, model_setup=None, data_loader=None,
                  seed=0):
-        self.config = config
+        self.config = plain(config)       # the reference's enum-typed TrainConfig or this build's
         self.callbacks = callbacks
         self.commands = commands
         self.model = model
@@ -44,17 +45,27 @@ class GenericTrainer:
     def start(self):
         cfg = self.config
         self.rank, self.world, local = init_from_env()
-        self.device = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device(cfg.train_device)
+        self.device = torch.device(f"cuda:{torch.cuda.current_device()}") if torch.cuda.is_available() \
+            else torch.device(str(cfg.train_device))
         if self.model is None:
             self.model = create.create_model(cfg, self.device, seed=self.seed)
+        from ..dataLoader.create import attach_cache_encoders, cache_ready, create_data_loader, has_concepts
+        # create.create_data_loader (create.py:391-431) when there is data to load: a latent cache at
+        # cache_dir or concepts to cache; step-level callers (bench, tests) pass batches to train_step
+        want_data = self.data_loader is None and (cache_ready(cfg) or has_concepts(cfg))
+        if want_data and not cache_ready(cfg):   # the model loader fills the caching encoders
+            attach_cache_encoders(self.model, cfg, self.device)
         self._load_weights()
+        if want_data:
+            self.data_loader = create_data_loader(cfg, self.model, self.device, self.rank, self.world)
         if self.model_setup is None:
             self.model_setup = create.create_model_setup(cfg, self.device, self.rank, self.world)
         self.model_setup.setup_model(self.model, cfg)
         self.model_setup.setup_train_device(self.model, cfg)
         self.parameters = self.model.parameters.parameters()
         if self.world > 1:
-            self.reducer = GradBucketReducer(self.model.train_store, bucket_bytes=cfg.dp_bucket_mb << 20)
+            self.reducer = GradBucketReducer(self.model.train_store, bucket_bytes=cfg.dp_bucket_mb << 20,
+                                             reduce_fp32=cfg.dp_reduce_fp32)
         approx = self.data_loader.get_data_set().approximate_length() if self.data_loader is not None else 1
         self.lr_scheduler = create_lr_scheduler(self.model.optimizer, cfg.learning_rate_scheduler,
                                                 cfg.learning_rate_warmup_steps, cfg.learning_rate_cycles,
@@ -155,6 +166,9 @@ class GenericTrainer:
         cfg, model, setup = self.config, self.model, self.model_setup
         tp = model.train_progress
         store = model.train_store
+        update = self._is_update_step(tp)
+        if self.reducer is not None:   # GA micro-steps accumulate locally; the update step's backward reduces
+            self.reducer.arm(update)
         loss = self.graphs.forward_backward(batch) if self.graphs is not None else None
         if loss is None:   # eager (or the first sight of a shape before its capture: trainer/step_graph.py)
             out = setup.predict(model, batch, cfg, tp)
@@ -163,7 +177,7 @@ class GenericTrainer:
             store.begin_backward()
             loss.backward()
             store.finish_backward()
-        if self._is_update_step(tp):
+        if update:
             if self.reducer is not None:
                 self.reducer.finish()
             if cfg.clip_grad_norm is not None:
@@ -180,6 +194,8 @@ class GenericTrainer:
     def train(self, log_every: int = 10, max_steps: int | None = None):
         cfg = self.config
         tp = self.model.train_progress
+        if self.data_loader is None:
+            raise RuntimeError("no data: set cache_dir to a latent cache or configure concepts")
         steps = 0
         for _epoch in range(tp.epoch, cfg.epochs):
             self.data_loader.get_data_set().start_next_epoch()

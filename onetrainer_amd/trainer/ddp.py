@@ -6,23 +6,35 @@ Buckets are contiguous slices of the flat grad buffer, formed in reverse layout 
 store is laid out in forward-execution order, so reverse order ~ the order backward finishes
 parameters).  Backward kernels write a parameter's gradient in place and call
 `store.mark_ready`; when every parameter of a bucket is ready its all-reduce is issued with
-async_op=True -- ProcessGroupNCCL orders it after the kernels already queued on the current
-stream and runs it on its own stream, overlapping the rest of backward.  `finish()` makes the
-current stream wait for all buckets.  The 1/world factor is folded into the loss gradient
-(BaseStableDiffusionXLSetup.calculate_loss), so a SUM all-reduce yields the global-batch mean.
+async_op=True from a dedicated issue stream that waits (by events) on BOTH the compute stream
+and the weight-gradient side stream (module/streams.py) -- neither compute stream is made to wait
+for the other or for the collective, so the reduce overlaps the rest of backward.  `finish()`
+makes the current stream wait for all buckets.  The 1/world factor is folded into the loss
+gradient (BaseStableDiffusionXLSetup.calculate_loss), so a SUM all-reduce yields the
+global-batch mean.
+
+Gradient accumulation: the reducer is armed only for the backward of an update step
+(`arm(update)` before every backward).  Earlier micro-steps accumulate locally into the grad
+store; the last micro-step's backward launches each bucket once, over the accumulated sum.
+
+Reduction dtype: bf16 in place (default: 2 B/param on the wire, the reference's grad dtype) or,
+with `reduce_fp32=True`, through an fp32 staging copy (4 B/param; one rounding to bf16 after the
+sum instead of one per ring hop).  tests/test_dp_gpu.py characterises both against a world-1
+step at the same global batch.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from ..module.streams import after_side
+from ..module import streams as S
 
 
 class GradBucketReducer:
-    def __init__(self, store, group=None, bucket_bytes: int = 256 << 20):
+    def __init__(self, store, group=None, bucket_bytes: int = 256 << 20, reduce_fp32: bool = False):
         self.store = store
         self.group = group
+        self.reduce_fp32 = reduce_fp32
         esz = store.grad.element_size()
         limit = max(1, bucket_bytes // esz)
         self.buckets = []         # (begin, end, names)
@@ -44,9 +56,43 @@ class GradBucketReducer:
             for n in names:
                 self.bucket_of[n] = bi
         self.pending = [len(b[2]) for b in self.buckets]
-        self.works = []
+        self.launched = [False] * len(self.buckets)
+        self.works = []           # (work, bucket index)
         self.enabled = True
+        self.staging = None       # fp32 copy of the flat grad buffer (reduce_fp32)
+        cuda = store.grad.is_cuda
+        self.issue_stream = torch.cuda.Stream(device=store.grad.device) if cuda else None
         store.ready_hooks.append(self._on_ready)
+
+    def arm(self, update_step: bool):
+        """before each backward: only an update step's backward reduces (GA micro-steps accumulate)."""
+        self.enabled = update_step
+        self.pending = [len(b[2]) for b in self.buckets]
+        self.launched = [False] * len(self.buckets)
+
+    def _launch(self, bi):
+        b, e, _ = self.buckets[bi]
+        g = self.store.grad[b:e]
+        self.launched[bi] = True
+        if self.issue_stream is None:
+            self.works.append((self._reduce(g, b, e), bi))
+            return
+        s = self.issue_stream
+        s.wait_stream(torch.cuda.current_stream())
+        side = S.side_stream()
+        if side is not None:
+            s.wait_stream(side)
+        with torch.cuda.stream(s):
+            self.works.append((self._reduce(g, b, e), bi))
+
+    def _reduce(self, g, b, e):
+        if not self.reduce_fp32:
+            return dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if self.staging is None:
+            self.staging = torch.empty(self.store.grad.numel(), dtype=torch.float32, device=g.device)
+        buf = self.staging[b:e]
+        buf.copy_(g)
+        return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _on_ready(self, names):
         if not self.enabled:
@@ -54,25 +100,22 @@ class GradBucketReducer:
         for n in names:
             bi = self.bucket_of[n]
             self.pending[bi] -= 1
-            if self.pending[bi] == 0:
-                b, e, _ = self.buckets[bi]
-                g = self.store.grad[b:e]
-                # ordered after both the main stream and the weight-gradient stream (module/streams.py)
-                self.works.append(after_side(lambda: dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
-                                                                     async_op=True)))
+            if self.pending[bi] == 0 and not self.launched[bi]:
+                self._launch(bi)
 
     def finish(self):
-        """reduce any bucket not yet launched (unused params), then wait for all of them."""
-        for bi, cnt in enumerate(self.pending):
-            if cnt > 0:
-                b, e, _ = self.buckets[bi]
-                g = self.store.grad[b:e]
-                self.works.append(after_side(lambda: dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
-                                                                     async_op=True)))
-        for w in self.works:
+        """reduce any bucket not yet launched (parameters without a gradient this step), then make
+        the current stream wait for every bucket."""
+        for bi in range(len(self.buckets)):
+            if not self.launched[bi]:
+                self._launch(bi)
+        for w, bi in self.works:
             w.wait()
+            if self.reduce_fp32:
+                b, e, _ = self.buckets[bi]
+                self.store.grad[b:e].copy_(self.staging[b:e])
         self.works = []
-        self.pending = [len(b[2]) for b in self.buckets]
+        self.arm(True)
 
 
 def init_from_env(backend: str | None = None):
@@ -83,8 +126,8 @@ def init_from_env(backend: str | None = None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("OTAMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if torch.cuda.is_available():
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(local if backend == "nccl" else local % max(1, torch.cuda.device_count()))
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local

@@ -101,8 +101,12 @@ class TrainConfig:
     continue_last_backup: bool = False
     rolling_backup: bool = False
     rolling_backup_count: int = 3
-    # build-only (not in the reference): data parallel + gradient bucket size
+    # concepts (TrainConfig.py:793-794): inline list of ConceptConfig dicts, else the concept file
+    concepts: list | None = None
+    concept_file_name: str = "training_concepts/concepts.json"
+    # build-only (not in the reference): data parallel gradient bucket size / fp32 reduction
     dp_bucket_mb: int = 256
+    dp_reduce_fp32: bool = False
     extra: dict = field(default_factory=dict)
 
     @staticmethod

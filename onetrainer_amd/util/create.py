@@ -8,6 +8,7 @@ import torch
 from ..model.StableDiffusionXLModel import NoiseScheduler, StableDiffusionXLModel
 from ..module import unet as U
 from ..util.lr_scheduler_util import create_lr_scheduler  # noqa: F401  (re-export)
+from .config.plain import plain
 
 SCALING = {"STABLE_DIFFUSION_XL_10_BASE": 0.13025, "STABLE_DIFFUSION_15": 0.18215}
 
@@ -19,6 +20,7 @@ def is_flux(model_type: str) -> bool:
 def create_model(config, device, seed=0, unet_config=None, prediction_type="epsilon", flux_config=None):
     """random-weight model of the configured architecture (weights from disk: SURVEY.md §8(f) #2).
     LoRA training keeps the base network frozen (no gradient buffer)."""
+    config = plain(config)
     mt = config.model_type
     if is_flux(mt):
         from ..model.FluxModel import FluxModel
@@ -44,6 +46,7 @@ def is_sd15(model_type: str) -> bool:
 
 def create_model_setup(config, train_device, dp_rank=0, dp_world=1):
     """ModelType x TrainingMethod -> plugin (create.py:285-353)."""
+    config = plain(config)
     if is_flux(config.model_type):
         if config.training_method == "LORA":
             from ..modelSetup.FluxLoRASetup import FluxLoRASetup as S

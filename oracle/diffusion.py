@@ -57,6 +57,20 @@ def timestep_discrete(num_train_timesteps, batch_size, generator, distribution="
     return t.int()
 
 
+def timestep_from_draws(draws, distribution="UNIFORM", num_train_timesteps=1000, min_strength=0.0, max_strength=1.0,
+                        shift=1.0):
+    """_get_timestep_discrete (ModelSetupNoiseMixin.py:91-118,155) applied to given draws: the U[0,1)
+    sample of torch.rand (UNIFORM) or the N(bias, weight+1) sample of torch.normal (LOGIT_NORMAL)."""
+    mn = int(num_train_timesteps * min_strength)
+    mx = int(num_train_timesteps * max_strength)
+    if distribution == "UNIFORM":
+        t = mn + (mx - mn) * draws
+    else:
+        t = draws.sigmoid() * (mx - mn) + mn
+    t = num_train_timesteps * shift * t / ((shift - 1) * t + num_train_timesteps)
+    return t.int()
+
+
 def timestep_continuous(batch_size, generator, **kw):
     d = timestep_discrete(10000, batch_size, generator, **kw) + 1
     return d.float() / 10000
@@ -120,9 +134,10 @@ def diffusion_losses(pred, target, loss_weight, t=None, betas=None, loss_weight_
 
 
 def flow_matching_losses(pred, target, loss_weight, t=None, loss_weight_fn="CONSTANT", num_timesteps=1000,
-                         mse_strength=1.0):
+                         mse_strength=1.0, batch_size_scale=1.0, ga_scale=1.0):
     mean_dim = list(range(1, pred.dim()))
     losses = torch.nn.functional.mse_loss(pred.float(), target.float(), reduction="none").mean(mean_dim) * mse_strength
+    losses = losses * batch_size_scale * ga_scale
     losses *= loss_weight.to(losses.dtype)
     if loss_weight_fn == "SIGMA":
         sig = torch.arange(1, num_timesteps + 1, dtype=torch.int32) / num_timesteps

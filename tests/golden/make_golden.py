@@ -74,6 +74,32 @@ def main():
     p = DiffProbe()
     rec["timestep_deterministic"] = p._get_timestep_discrete(1000, True, torch.Generator().manual_seed(0), 4, cfg).numpy()
 
+    # ---- 1b. timestep transform on recorded draws (feeds the HIP kernel's injected-draw path) ---------
+    # the draw the reference makes inside _get_timestep_discrete is re-made from the same seed
+    # (torch.rand / torch.normal with the same generator state), then the reference maps it
+    n_draw = 512
+    for name, dist, extra in (("uniform", "UNIFORM", {}), ("uniform_shift3", "UNIFORM", {"timestep_shift": 3.0}),
+                              ("uniform_range", "UNIFORM", {"min_noising_strength": 0.1, "max_noising_strength": 0.9}),
+                              ("logitnormal", "LOGIT_NORMAL", {}),
+                              ("logitnormal_b", "LOGIT_NORMAL", {"noising_bias": 0.5, "noising_weight": 0.3}),
+                              ("logitnormal_shift", "LOGIT_NORMAL", {"timestep_shift": 2.5})):
+        c = TrainConfig.default_values()
+        c.train_device = "cpu"
+        c.timestep_distribution = TimestepDistribution[dist]
+        for k, v in extra.items():
+            setattr(c, k, v)
+        g = torch.Generator(device="cpu").manual_seed(42)
+        t = DiffProbe()._get_timestep_discrete(1000, False, g, n_draw, c)
+        g = torch.Generator(device="cpu").manual_seed(42)
+        if dist == "UNIFORM":
+            draws = torch.rand(n_draw, generator=g)
+        else:
+            draws = torch.normal(c.noising_bias, c.noising_weight + 1.0, size=(n_draw,), generator=g)
+        rec[f"tsinj_{name}_draws"] = draws.numpy()
+        rec[f"tsinj_{name}_t"] = t.numpy()
+        rec[f"tsinj_{name}_cfg"] = np.array([c.min_noising_strength, c.max_noising_strength, c.timestep_shift,
+                                             c.noising_bias, c.noising_weight], dtype=np.float64)
+
     # ---- 2. add noise -------------------------------------------------------------------------------
     torch.manual_seed(123)
     betas = torch.linspace(0.00085 ** 0.5, 0.012 ** 0.5, 1000, dtype=torch.float32) ** 2

@@ -64,6 +64,54 @@ def test_bucket_allreduce_gloo_world2():
     assert res == {0: "ok", 1: "ok"}, res
 
 
+def _worker_ga(rank, world, port, q, reduce_fp32):
+    """gradient accumulation 2 (trainer/GenericTrainer.train_step): the reducer is armed only for the
+    update step's backward; the first micro-step accumulates locally, no bucket is reduced twice."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = FlatParamStore(SPECS, torch.bfloat16 if reduce_fp32 else torch.float32, "cpu")
+        red = GradBucketReducer(st, bucket_bytes=2048, reduce_fp32=reduce_fp32)
+        for window in range(2):
+            for micro in range(2):
+                red.arm(micro == 1)
+                for i, (n, s, _) in enumerate(SPECS):
+                    g = st.params[n].grad
+                    v = float(rank + 1 + i % 8 + 10 * micro + 20 * window)   # sums stay exact in bf16
+                    if micro == 0:
+                        g.fill_(v)
+                    else:
+                        g.add_(v)
+                for n in reversed(st.order):
+                    st.mark_ready([n])
+                if micro == 0:
+                    assert not red.works, "a GA micro-step launched an all-reduce"
+            red.finish()
+            for i, (n, s, _) in enumerate(SPECS):
+                exp = sum(2 * (r + 1 + i % 8 + 20 * window) + 10 for r in range(world))
+                assert torch.all(st.params[n].grad.float() == exp), (n, st.params[n].grad[:3], exp)
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("reduce_fp32", [False, True])
+def test_bucket_allreduce_grad_accumulation_gloo_world2(reduce_fp32):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_ga, args=(r, 2, port, q, reduce_fp32)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res
+
+
 def test_bucket_partition_is_contiguous_and_complete():
     st = FlatParamStore(SPECS, torch.bfloat16, "cpu")
     if not dist.is_available():

@@ -1,0 +1,72 @@
+"""Data-parallel equivalence: two ranks at b=1 each == one rank at b=2.
+
+The ranks are fresh child processes on the one GPU of the test box (torch.distributed 'gloo'
+with HIP tensors: RCCL cannot put two ranks on one device), each running
+tests/workers/dp_step.py; the world-1 reference runs the whole global batch.  Compared after one
+step (GenericTrainer.train_step: predict -> loss -> backward + bucketed all-reduce -> clip ->
+AdamW, stochastic rounding off):
+  * loss: mean over ranks vs the world-1 loss, rtol 1e-5 (fp32; summation order only);
+  * clip total norm: rtol 2e-3;
+  * reduced gradients: global cosine >= 0.9999 and relative L2 error <= 1e-2 -- the bf16 bucket
+    reduction rounds each rank's partial and the sum (world-1 rounds the fp32 wgrad once); the fp32
+    staging reduction (dp_reduce_fp32) is held to the same bound and reported next to it;
+  * post-step bf16 parameters: <= 1e-3 of the elements differ (AdamW's first step moves every
+    element by ~lr * sign(g); a difference needs a near-zero gradient whose sign flips).
+"""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+WORKER = Path(__file__).parent / "workers" / "dp_step.py"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(tmp, world, fp32=False):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    outs, procs = [], []
+    port = _port()
+    for r in range(world):
+        e = dict(env)
+        if world > 1:
+            e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                     MASTER_PORT=str(port), OTAMD_DIST_BACKEND="gloo")
+        out = tmp / f"w{world}_{int(fp32)}_r{r}.pt"
+        cmd = [sys.executable, str(WORKER), "--global-batch", "2", "--out", str(out)] + (["--fp32-reduce"] if fp32 else [])
+        procs.append(subprocess.Popen(cmd, env=e))
+        outs.append(out)
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    return [torch.load(o, weights_only=True) for o in outs]
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_dp2_equals_single_rank_global_batch(tmp_path, fp32):
+    ref = _run(tmp_path, 1)[0]
+    r0, r1 = _run(tmp_path, 2, fp32)
+    loss_dp = (r0["loss"] + r1["loss"]) / 2
+    torch.testing.assert_close(loss_dp, ref["loss"], rtol=1e-5, atol=0)
+    torch.testing.assert_close(r0["norm"], ref["norm"], rtol=2e-3, atol=0)
+    assert torch.equal(r0["grad"], r1["grad"]) and torch.equal(r0["param"], r1["param"])   # replicas identical
+    g, gr = r0["grad"], ref["grad"]
+    cos = torch.nn.functional.cosine_similarity(g, gr, dim=0).item()
+    rel = ((g - gr).norm() / gr.norm()).item()
+    diff = (r0["param"] != ref["param"]).float().mean().item()
+    print(f"dp2 vs dp1 ({'fp32' if fp32 else 'bf16'} reduce): grad cos {cos:.7f} rel-L2 {rel:.3e} "
+          f"params differing {diff:.2e} loss {loss_dp.tolist()} vs {ref['loss'].tolist()}")
+    assert cos >= 0.9999 and rel <= 1e-2
+    assert diff <= 1e-3

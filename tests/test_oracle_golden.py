@@ -121,3 +121,16 @@ def test_sr_bits_uniform():
     for seed in (0, 42, 0xFFFFFFFFFFFFFFFF):
         got = OA.sr_bits(seed, idx)
         assert [int(v) for v in got] == [_sr_bits_py(seed, int(i)) for i in idx]
+
+
+TSINJ = {"uniform": "UNIFORM", "uniform_shift3": "UNIFORM", "uniform_range": "UNIFORM", "logitnormal": "LOGIT_NORMAL",
+         "logitnormal_b": "LOGIT_NORMAL", "logitnormal_shift": "LOGIT_NORMAL"}
+
+
+@pytest.mark.parametrize("name", list(TSINJ))
+def test_timestep_transform_on_draws(name):
+    """oracle.timestep_from_draws on the reference's own draws == the reference's timesteps (bit-exact)."""
+    mn, mx, shift, _bias, _w = G[f"tsinj_{name}_cfg"]
+    t = OD.timestep_from_draws(torch.from_numpy(G[f"tsinj_{name}_draws"]), TSINJ[name], 1000, float(mn), float(mx),
+                               float(shift))
+    assert np.array_equal(t.numpy(), G[f"tsinj_{name}_t"])
