@@ -284,10 +284,11 @@ int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s)
 int otamd_noise(void* out, int f32, long long n, long long offset, unsigned long long seed, hipStream_t s);
 
 /* replaces: ModelSetupNoiseMixin._get_timestep_discrete (ModelSetupNoiseMixin.py:51-155), UNIFORM (dist 0) and
-   LOGIT_NORMAL (dist 1) with static shift.  draws (nullable): injected per-sample draws instead of Philox --
-   the U[0,1) sample (UNIFORM) or the N(bias, weight+1) sample (LOGIT_NORMAL) of the reference's generator. */
+   LOGIT_NORMAL (dist 1) with static shift.  min_t / max_t = int(num_train_timesteps * min/max_noising_strength)
+   (:69-70).  draws (nullable): injected per-sample draws instead of Philox -- the U[0,1) sample (UNIFORM) or the
+   N(bias, weight+1) sample (LOGIT_NORMAL) of the reference's generator. */
 int otamd_timesteps(int* out, int n, long long sample0, unsigned long long seed, int dist, int
-    num_train_timesteps, float min_s, float max_s, float shift, float bias, float weight, const float* draws,
+    num_train_timesteps, int min_t, int max_t, float shift, float bias, float weight, const float* draws,
     hipStream_t s);
 
 /* replaces: BaseStableDiffusionXLSetup.predict scale + _add_noise_discrete + get_velocity (BaseStableDiffusionXLSetup.py:214-236,277-291; ModelSetupDiffusionMixin.py:15-38) */

@@ -140,7 +140,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_flux_pack": [VP, VP, I, I, I, I, I, I, VP],
     # diffusion.hip
     "otamd_noise": [VP, I, LL, LL, U64, VP],
-    "otamd_timesteps": [VP, I, LL, U64, I, I, F, F, F, F, F, VP, VP],
+    "otamd_timesteps": [VP, I, LL, U64, I, I, I, I, F, F, F, VP, VP],
     "otamd_ddpm_prologue": [VP, VP, I, VP, VP, VP, VP, F, I, LL, I, I, VP, VP, I, VP, VP],
     "otamd_flow_prologue": [VP, VP, I, VP, F, F, I, I, LL, I, I, VP, VP, VP],
     "otamd_mse_loss": [VP, I, VP, I, I, LL, I, F, F, VP, VP, VP, VP, I, F, I, I, F, VP, LL, VP, VP, VP, VP],

@@ -68,13 +68,13 @@ __global__ void noise_kernel(void* out, int f32, long long n, long long offset, 
 // dist 0 = UNIFORM, 1 = LOGIT_NORMAL (ModelSetupNoiseMixin.py:91-118).  draws != nullptr injects the
 // random draw of each sample instead of Philox (parity tests): UNIFORM -> the U[0,1) sample of
 // torch.rand, LOGIT_NORMAL -> the N(bias, weight + 1) sample of torch.normal (bias / weight unused).
+// mn / mx = int(num_train_timesteps * min/max_noising_strength), computed by the host in double like
+// the reference's python ints (ModelSetupNoiseMixin.py:69-70).
 __global__ void timestep_kernel(int* out, int n, long long sample0, unsigned long long seed, int dist,
-                                int num_train_timesteps, float min_s, float max_s, float shift, float bias,
+                                int num_train_timesteps, int mn, int mx, float shift, float bias,
                                 float weight, const float* draws) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  // int(num_train_timesteps * strength): the python product is a double, truncated toward zero
-  const int mn = (int)((double)num_train_timesteps * (double)min_s), mx = (int)((double)num_train_timesteps * (double)max_s);
   float t;
   if (dist == 0) {
     const float u = draws ? draws[i] : philox_uniform(seed, 2u, (uint64_t)(sample0 + i));
@@ -251,10 +251,12 @@ OTAMD_API int otamd_noise(void* out, int f32, long long n, long long offset, uns
   return OTAMD_OK;
 }
 OTAMD_API int otamd_timesteps(int* out, int n, long long sample0, unsigned long long seed, int dist,
-                              int num_train_timesteps, float min_s, float max_s, float shift, float bias, float weight,
+                              int num_train_timesteps, int min_t, int max_t, float shift, float bias, float weight,
                               const float* draws, hipStream_t s) {
-  if (!out || n <= 0 || num_train_timesteps <= 0 || (dist != 0 && dist != 1)) return OTAMD_EINVAL;
-  timestep_kernel<<<(n + 63) / 64, 64, 0, s>>>(out, n, sample0, seed, dist, num_train_timesteps, min_s, max_s, shift,
+  if (!out || n <= 0 || num_train_timesteps <= 0 || (dist != 0 && dist != 1) || min_t < 0 || max_t < min_t ||
+      max_t > num_train_timesteps)
+    return OTAMD_EINVAL;
+  timestep_kernel<<<(n + 63) / 64, 64, 0, s>>>(out, n, sample0, seed, dist, num_train_timesteps, min_t, max_t, shift,
                                                bias, weight, draws);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;

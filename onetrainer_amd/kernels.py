@@ -846,9 +846,10 @@ def timesteps(n, seed, sample0=0, dist=0, num_train_timesteps=1000, min_s=0.0, m
     if draws is not None:
         _req(draws.dtype == F32 and draws.numel() == n and draws.is_contiguous() and draws.device == out.device,
              "timestep draws: f32 [n] on the output's device")
-    check(lib().otamd_timesteps(_p(out), n, sample0, seed & 0xFFFFFFFFFFFFFFFF, dist, num_train_timesteps,
-                                float(min_s), float(max_s), float(shift), float(bias), float(weight), _p(draws),
-                                stream_handle()), "otamd_timesteps")
+    mn, mx = int(num_train_timesteps * min_s), int(num_train_timesteps * max_s)   # python ints, like :69-70
+    check(lib().otamd_timesteps(_p(out), n, sample0, seed & 0xFFFFFFFFFFFFFFFF, dist, num_train_timesteps, mn, mx,
+                                float(shift), float(bias), float(weight), _p(draws), stream_handle()),
+          "otamd_timesteps")
     return out
 
 

@@ -31,6 +31,7 @@ class BaseFluxSetup:
         self.debug_mode = debug_mode
         self.dp_rank = dp_rank
         self.dp_world = dp_world
+        self.graph_inputs = None   # injected (noise NHWC, timestep int32): parity tests
 
     @staticmethod
     def _nhwc_latent(lat: torch.Tensor) -> torch.Tensor:
@@ -71,17 +72,20 @@ class BaseFluxSetup:
         latent = self._nhwc_latent(batch["latent_image"])
         B, h, w, C = latent.shape
         pooled, ehs = self._text(batch, config, rand, B)
-        sample0 = self.dp_rank * B
-        noise = K.noise(latent.shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=latent.dtype,
-                        device=latent.device)
         N = model.noise_scheduler.config["num_train_timesteps"]
-        if deterministic:
-            timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=latent.device)
+        if self.graph_inputs is not None:
+            noise, timestep = self.graph_inputs
         else:
-            timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=timestep_plan(config), num_train_timesteps=N,
-                                   min_s=config.min_noising_strength, max_s=config.max_noising_strength,
-                                   shift=self._shift(config, h, w), bias=config.noising_bias,
-                                   weight=config.noising_weight, device=latent.device)
+            sample0 = self.dp_rank * B
+            noise = K.noise(latent.shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=latent.dtype,
+                            device=latent.device)
+            if deterministic:
+                timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=latent.device)
+            else:
+                timestep = K.timesteps(B, seed=batch_seed, sample0=sample0, dist=timestep_plan(config),
+                                       num_train_timesteps=N, min_s=config.min_noising_strength, max_s=config.max_noising_strength,
+                                       shift=self._shift(config, h, w), bias=config.noising_bias,
+                                       weight=config.noising_weight, device=latent.device)
         vc = model.vae.config
         model_in, target = K.flow_prologue(latent, noise, timestep, vc["scaling_factor"], vc["shift_factor"], N,
                                            cpad=C)

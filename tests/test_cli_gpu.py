@@ -19,11 +19,11 @@ def test_train_script_runs_reference_config(dev, tmp_path):
     from onetrainer_amd.module import vae as V
     torch.manual_seed(0)
     enc = V.AutoencoderKLEncoder(V.tiny_vae_config(), dev, seed=1)
-    shapes = [(128, 128), (128, 128), (96, 160), (96, 160)]
+    shapes = [(128, 128), (128, 128), (128, 192), (128, 192)]   # SD 1.5 latents: multiples of 8
     samples = [{"image": torch.rand(3, h, w), "text": {"text_encoder_hidden_state": torch.randn(77, 768).bfloat16()}}
                for h, w in shapes]
     cache = tmp_path / "cache"
-    LatentCacheWriter(lambda im: enc.encode(im), str(cache), AspectBucketing(128, 8), dev, encode_batch=2).write(samples)
+    LatentCacheWriter(lambda im: enc.encode(im), str(cache), AspectBucketing(128, 64), dev, encode_batch=2).write(samples)
     cfg = {"__version": 6, "model_type": "STABLE_DIFFUSION_15", "training_method": "FINE_TUNE",
            "cache_dir": str(cache), "batch_size": 2, "epochs": 1, "learning_rate": 1e-5,
            "learning_rate_warmup_steps": 0, "workspace_dir": str(tmp_path / "ws"), "train_dtype": "BFLOAT_16",

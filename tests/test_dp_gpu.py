@@ -10,8 +10,10 @@ AdamW, stochastic rounding off):
   * reduced gradients: global cosine >= 0.9999 and relative L2 error <= 1e-2 -- the bf16 bucket
     reduction rounds each rank's partial and the sum (world-1 rounds the fp32 wgrad once); the fp32
     staging reduction (dp_reduce_fp32) is held to the same bound and reported next to it;
-  * post-step bf16 parameters: <= 1e-3 of the elements differ (AdamW's first step moves every
-    element by ~lr * sign(g); a difference needs a near-zero gradient whose sign flips).
+  * post-step bf16 parameters: <= 1e-2 of the elements differ, each by at most 2 lr (AdamW's first
+    step moves every element by ~lr * g / (|g| + eps); the per-rank partial sums move a gradient by
+    ~1 bf16 ulp, which flips the rounding of some updated parameters (<= 1 ulp of the parameter) or
+    the sign of a near-zero g (<= 2 lr)).
 """
 import os
 import socket
@@ -66,7 +68,11 @@ def test_dp2_equals_single_rank_global_batch(tmp_path, fp32):
     cos = torch.nn.functional.cosine_similarity(g, gr, dim=0).item()
     rel = ((g - gr).norm() / gr.norm()).item()
     diff = (r0["param"] != ref["param"]).float().mean().item()
+    pa, pr = r0["param"].float(), ref["param"].float()
+    ulp = torch.exp2(torch.floor(torch.log2(pr.abs().clamp_min(1e-30))) - 7)      # bf16 spacing at |p|
+    excess = ((pa - pr).abs() - (2 * 1e-4 + ulp)).max().item()
+    dmax = (pa - pr).abs().max().item()
     print(f"dp2 vs dp1 ({'fp32' if fp32 else 'bf16'} reduce): grad cos {cos:.7f} rel-L2 {rel:.3e} "
-          f"params differing {diff:.2e} loss {loss_dp.tolist()} vs {ref['loss'].tolist()}")
+          f"params differing {diff:.2e} (max {dmax:.2e}) loss {loss_dp.tolist()} vs {ref['loss'].tolist()}")
     assert cos >= 0.9999 and rel <= 1e-2
-    assert diff <= 1e-3
+    assert diff <= 1e-2 and excess <= 0

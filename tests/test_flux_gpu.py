@@ -200,7 +200,8 @@ def test_flux_lora_train_steps(dev):
     ol = OracleLoRA(om, 8, 8.0, prefix="lora_transformer")
     ol.load_state_dict({k: v.float().cpu() for k, v in model.transformer_lora.state_dict().items()
                         if not k.endswith(".alpha")})
-    opt = torch.optim.AdamW(ol.parameters(), lr=3e-4, weight_decay=1e-2, foreach=False)
+    from _oracle_opt import OracleF32AdamW
+    opt = OracleF32AdamW(ol.parameters(), lr=3e-4, weight_decay=1e-2)   # fp32 adapters, pinned AdamW restatement
     res = 128
     batch = synthetic_flux_batch(2, res, res, dev, seed=1, t5_dim=fcfg.joint_attention_dim,
                                  pooled_dim=fcfg.pooled_projection_dim, text_len=9)
@@ -223,11 +224,9 @@ def test_flux_lora_train_steps(dev):
         pred = OF.unpack_latents(pred, h, w)
         loss = ((pred - (eps - x0)) ** 2).mean()
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(ol.parameters(), 1.0)
         opt.step()
-        opt.zero_grad()
         ref.append(loss.item())
     print("flux lora losses hip", ours, "oracle", ref)
-    assert abs(ours[0] - ref[0]) <= 1e-3 * abs(ref[0]) + 1e-4, (ours, ref)
-    assert abs(ours[1] - ref[1]) <= 2e-2 * abs(ref[1]), (ours, ref)
+    for a, b in zip(ours, ref):
+        assert abs(a - b) <= 1e-3 * abs(b), (ours, ref)
     assert torch.equal(model.transformer.store.data, base0)

@@ -13,6 +13,8 @@ from onetrainer_amd.util.config.TrainConfig import TrainConfig
 from oracle import diffusion as OD
 from oracle import unet as OU
 
+from _oracle_opt import OracleBF16AdamW
+
 pytestmark = pytest.mark.gpu
 
 
@@ -36,7 +38,7 @@ def test_train_step_matches_oracle(dev, ptype):
     tr.start()
     res = 128
     batch = synthetic_sdxl_batch(2, res, res, dev, seed=1, te1_dim=48, te2_dim=48, pooled_dim=64)
-    opt = torch.optim.AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2, foreach=False)
+    opt = OracleBF16AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2)   # bf16 p/m/v like the reference
     betas = OD.scaled_linear_betas()
     lat = batch["latent_image"].cpu().permute(0, 3, 1, 2).float()
     ehs = torch.cat([batch["text_encoder_1_hidden_state"], batch["text_encoder_2_hidden_state"]], -1).float().cpu()
@@ -57,14 +59,11 @@ def test_train_step_matches_oracle(dev, ptype):
         target = eps if ptype == "epsilon" else OD.get_velocity(x0, eps, tc, betas)
         loss = OD.diffusion_losses(pred, target, torch.ones(2)).mean()
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(om.parameters(), 1.0)
-        opt.step()
-        opt.zero_grad()
+        opt.step()                                   # bf16 clip_grad_norm_ + patched AdamW (pinned oracle)
         ref.append(loss.item())
     print("losses hip", ours, "oracle", ref)
-    assert abs(ours[0] - ref[0]) <= 1e-3 * abs(ref[0]), (ours, ref)
-    for a, b in zip(ours[1:], ref[1:]):
-        assert abs(a - b) <= 2e-2 * abs(b), (ours, ref)
+    for a, b in zip(ours, ref):                      # north star: loss within rtol 1e-3 of the reference
+        assert abs(a - b) <= 1e-3 * abs(b), (ours, ref)
 
 
 def test_sd15_train_step_matches_oracle(dev):
@@ -87,7 +86,7 @@ def test_sd15_train_step_matches_oracle(dev):
     assert type(tr.model_setup).__name__ == "StableDiffusionFineTuneSetup"
     res = 128
     batch = synthetic_sdxl_batch(2, res, res, dev, seed=1, te1_dim=96, sdxl=False, scaling_factor=0.18215)
-    opt = torch.optim.AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2, foreach=False)
+    opt = OracleBF16AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2)
     betas = OD.scaled_linear_betas()
     lat = batch["latent_image"].cpu().permute(0, 3, 1, 2).float()
     ehs = batch["text_encoder_hidden_state"].float().cpu()
@@ -103,13 +102,11 @@ def test_sd15_train_step_matches_oracle(dev):
         pred = om(xt.bfloat16().float(), tc, ehs)
         loss = OD.diffusion_losses(pred, eps, torch.ones(2)).mean()
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(om.parameters(), 1.0)
         opt.step()
-        opt.zero_grad()
         ref.append(loss.item())
     print("sd15 losses hip", ours, "oracle", ref)
-    assert abs(ours[0] - ref[0]) <= 1e-3 * abs(ref[0]), (ours, ref)
-    assert abs(ours[1] - ref[1]) <= 2e-2 * abs(ref[1]), (ours, ref)
+    for a, b in zip(ours, ref):
+        assert abs(a - b) <= 1e-3 * abs(b), (ours, ref)
 
 
 def test_dp_noise_slices_match_global(dev):
