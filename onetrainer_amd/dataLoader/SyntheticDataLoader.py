@@ -18,7 +18,7 @@ def synthetic_sdxl_batch(batch_size, height, width, device, seed=0, latent_dtype
     h, w = height // 8, width // 8
     lat = (torch.randn(batch_size, h, w, 4, generator=g) / scaling_factor).to(device, latent_dtype)
     b = {
-        "latent_image": lat,
+        "latent_image": lat.permute(0, 3, 1, 2),   # the reference's NCHW contract, channels-last storage
         "text_encoder_1_hidden_state": torch.randn(batch_size, text_len, te1_dim, generator=g).to(device, torch.bfloat16),
         "loss_weight": torch.ones(batch_size, device=device),
         "concept_type": ["STANDARD"] * batch_size,
@@ -69,7 +69,7 @@ def synthetic_flux_batch(batch_size, height, width, device, seed=0, latent_dtype
     h, w = height // 8, width // 8
     lat = (torch.randn(batch_size, h, w, channels, generator=g) / scaling_factor + shift_factor).to(device, latent_dtype)
     return {
-        "latent_image": lat,
+        "latent_image": lat.permute(0, 3, 1, 2),   # NCHW view of channels-last storage
         "text_encoder_1_pooled_state": torch.randn(batch_size, pooled_dim, generator=g).to(device, torch.bfloat16),
         "text_encoder_2_hidden_state": torch.randn(batch_size, text_len, t5_dim, generator=g).to(device, torch.bfloat16),
         "loss_weight": torch.ones(batch_size, device=device),

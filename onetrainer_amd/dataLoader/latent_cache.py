@@ -160,6 +160,8 @@ class LatentCacheDataLoader:
                 dev[k] = tuple(t.to(self.device, non_blocking=True) for t in v)
             else:
                 dev[k] = v.to(self.device, non_blocking=True)
+        # the reference's [B, C, h, w] contract, as a view of the cached channels-last (NHWC) storage
+        dev["latent_image"] = dev["latent_image"].permute(0, 3, 1, 2)
         dev["concept_type"] = ["STANDARD"] * dev["latent_image"].shape[0]
         return dev
 

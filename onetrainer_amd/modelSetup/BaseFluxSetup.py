@@ -4,7 +4,7 @@ Drop-in for modules/modelSetup/BaseFluxSetup.py:193-390 with the math of ModelSe
 (noise; LOGIT_NORMAL / UNIFORM timesteps, static or dynamic shift), ModelSetupFlowMatchingMixin.py:14-39
 (sigma = (t + 1) / N, x_t = sigma noise + (1 - sigma) x0), FluxModel.pack/unpack_latents and
 ModelSetupDiffusionLossMixin._flow_matching_losses (unmasked MSE, flow target noise - x0):
-  * latents arrive NHWC [B, h, w, 16] (this build's cache) or NCHW [B, 16, h, w];
+  * latents arrive [B, 16, h, w] (this build's loaders: a view of channels-last storage);
   * one prologue kernel does the shift / scale, the noising and the flow target;
   * the transformer gets t / 1000 and guidance = prior.guidance_scale, like the reference.
 Batch contract: text_encoder_1_pooled_state [B, 768] (CLIP pooled), text_encoder_2_hidden_state
@@ -35,9 +35,8 @@ class BaseFluxSetup:
 
     @staticmethod
     def _nhwc_latent(lat: torch.Tensor) -> torch.Tensor:
-        if lat.dim() == 4 and lat.shape[1] == 16 and lat.shape[-1] != 16:
-            lat = lat.permute(0, 2, 3, 1)
-        return lat.contiguous()
+        """[B, 16, h, w] (reference contract; channels-last storage from this build's loaders) -> NHWC."""
+        return lat.permute(0, 2, 3, 1).contiguous()
 
     def _text(self, batch, config, rand, B):
         """FluxModel.encode_text with cached outputs: per-encoder dropout masks from Random(seed)."""

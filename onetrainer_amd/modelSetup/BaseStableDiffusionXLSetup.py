@@ -8,7 +8,8 @@ ModelSetupDiffusionLossMixin.py:119-279 done by csrc/diffusion.hip:
   * DDPM noising + target (epsilon / v_prediction) in one prologue kernel;
   * unmasked MSE (+ MIN_SNR_GAMMA / DEBIASED_ESTIMATION / P2 weights, loss_weight, scalers).
 Batch contract as the reference's data loader (StableDiffusionXLBaseDataLoader.py:174-209),
-except that `latent_image` may be NHWC [B,h,w,4] (this build's loader) or NCHW [B,4,h,w].
+with `latent_image` [B, 4, h, w]; this build's loaders hand it over as a view of channels-last
+storage, so the kernels' NHWC layout costs no copy.
 """
 from __future__ import annotations
 
@@ -82,9 +83,9 @@ class BaseStableDiffusionXLSetup:
     # ------------------------------------------------------------------------------------------
     @staticmethod
     def _nhwc_latent(lat: torch.Tensor) -> torch.Tensor:
-        if lat.dim() == 4 and lat.shape[1] == 4 and lat.shape[-1] != 4:
-            lat = lat.permute(0, 2, 3, 1)
-        return lat.contiguous()
+        """batch latent [B, C, h, w] (the reference contract) -> NHWC for the kernels: free when the
+        tensor is a channels-last view (this build's loaders), one relayout copy otherwise (mgds)."""
+        return lat.permute(0, 2, 3, 1).contiguous()
 
     def _text(self, model, batch, config, rand, B):
         config = plain(config)

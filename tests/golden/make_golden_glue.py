@@ -139,6 +139,11 @@ def main():
             return sa * noise - sb * sample
 
     rec: dict = {}
+    from modules.util.DiffusionScheduleCoefficients import DiffusionScheduleCoefficients
+    co = DiffusionScheduleCoefficients.from_betas(betas)   # the tables _add_noise_discrete / get_velocity index
+    rec["ddpm_tables"] = {"alphas_cumprod": co.alphas_cumprod, "sqrt_alphas_cumprod": co.sqrt_alphas_cumprod,
+                          "sqrt_one_minus_alphas_cumprod": co.sqrt_one_minus_alphas_cumprod}
+    assert torch.equal(co.alphas_cumprod, acp)
 
     # ---- #5 SDXL predict + loss ------------------------------------------------------------------
     class RecUNet(torch.nn.Module):

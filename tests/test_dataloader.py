@@ -71,9 +71,10 @@ def test_latent_cache_round_trip(tmp_path):
     for batch in dl.get_data_loader():
         lat = batch["latent_image"]
         ch, cw = batch["crop_resolution"][0][0].item(), batch["crop_resolution"][1][0].item()
-        assert lat.shape == (1, ch // 8, cw // 8, 4) and lat.dtype == torch.float32
+        assert lat.shape == (1, 4, ch // 8, cw // 8) and lat.dtype == torch.float32
+        assert lat.permute(0, 2, 3, 1).is_contiguous()       # NCHW view of channels-last storage
         assert batch["text_encoder_hidden_state"].shape == (1, 77, 16)
-        assert torch.count_nonzero(lat[..., 3]) == 0
+        assert torch.count_nonzero(lat[:, 3]) == 0
         got += 1
     assert got == len(shapes)
     # two ranks of a global batch of 2 read disjoint halves of the same batches

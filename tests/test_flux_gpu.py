@@ -207,7 +207,7 @@ def test_flux_lora_train_steps(dev):
                                  pooled_dim=fcfg.pooled_projection_dim, text_len=9)
     base0 = model.transformer.store.data.clone()
     h = w = res // 8
-    lat = batch["latent_image"].cpu().permute(0, 3, 1, 2).float()
+    lat = batch["latent_image"].cpu().float()
     x0 = (lat - 0.1159) * 0.3611
     ours, ref = [], []
     for step in range(2):

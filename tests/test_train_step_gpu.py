@@ -40,7 +40,7 @@ def test_train_step_matches_oracle(dev, ptype):
     batch = synthetic_sdxl_batch(2, res, res, dev, seed=1, te1_dim=48, te2_dim=48, pooled_dim=64)
     opt = OracleBF16AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2)   # bf16 p/m/v like the reference
     betas = OD.scaled_linear_betas()
-    lat = batch["latent_image"].cpu().permute(0, 3, 1, 2).float()
+    lat = batch["latent_image"].cpu().float()
     ehs = torch.cat([batch["text_encoder_1_hidden_state"], batch["text_encoder_2_hidden_state"]], -1).float().cpu()
     te = batch["text_encoder_2_pooled_state"].float().cpu()
     tid = torch.tensor([[res, res, 0, 0, res, res]] * 2, dtype=torch.float32)
@@ -88,7 +88,7 @@ def test_sd15_train_step_matches_oracle(dev):
     batch = synthetic_sdxl_batch(2, res, res, dev, seed=1, te1_dim=96, sdxl=False, scaling_factor=0.18215)
     opt = OracleBF16AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2)
     betas = OD.scaled_linear_betas()
-    lat = batch["latent_image"].cpu().permute(0, 3, 1, 2).float()
+    lat = batch["latent_image"].cpu().float()
     ehs = batch["text_encoder_hidden_state"].float().cpu()
     ours, ref = [], []
     for step in range(2):
