@@ -92,7 +92,10 @@ class BaseFluxSetup:
         guidance = None
         if model.transformer.config["guidance_embeds"]:
             guidance = torch.full((B,), float(config.prior.guidance_scale), dtype=torch.float32, device=latent.device)
-        pred_tok = model.transformer(tokens, timestep.float() / 1000, guidance, pooled, ehs, h, w)
+        # timestep / 1000 (BaseFluxSetup.py:291) as an IEEE division: torch's tensor / python-scalar on the GPU
+        # multiplies by the reciprocal (1 ulp off in places); a tensor divisor divides
+        t_model = timestep.float() / torch.full((B,), 1000.0, dtype=torch.float32, device=latent.device)
+        pred_tok = model.transformer(tokens, t_model, guidance, pooled, ehs, h, w)
         pred = O.UnpackFn.apply(pred_tok, B, h, w, C)
         # reference contract: [B, 16, h, w] (BaseFluxSetup.py:301-307); views of the NHWC kernel tensors
         return {"loss_type": "target", "timestep": timestep, "predicted": pred.permute(0, 3, 1, 2),

@@ -19,11 +19,26 @@ def main() -> None:
     ap.add_argument("out")
     ap.add_argument("--steps-kernel", default="adamw_bf16")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--all", action="store_true", help="every dispatch of the run (default: the timed steps only)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = c.execute("select name, count(*), sum(duration) from kernels group by name order by sum(duration) desc").fetchall()
+    if a.all:
+        rows = c.execute("select name, count(*), sum(duration) from kernels group by name order by sum(duration) desc").fetchall()
+        steps = sum(r[1] for r in rows if a.steps_kernel in r[0]) or 1
+    else:
+        # only whole steps between optimizer launches, skipping the first window (model init, first-shape
+        # planning, warm-up) and the last one (bench.py's extra roofline step runs after the timed steps)
+        ev = c.execute("select name, start, end from kernels order by start").fetchall()
+        marks = [s for n, s, e in ev if a.steps_kernel in n]
+        lo, hi = marks[1], marks[-2]
+        steps = max(1, len(marks) - 3)
+        agg = {}
+        for n, s, e in ev:
+            if lo < s <= hi:
+                cnt, d = agg.get(n, (0, 0))
+                agg[n] = (cnt + 1, d + (e - s))
+        rows = sorted(((n, cnt, d) for n, (cnt, d) in agg.items()), key=lambda r: -r[2])
     total = sum(r[2] for r in rows)
-    steps = sum(r[1] for r in rows if a.steps_kernel in r[0]) or 1
     with open(a.out, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "CallsPerStep", "MsPerStep"])
