@@ -318,6 +318,13 @@ int otamd_mse_grad(const void* pred, int cpad, const void* target, int tgt_f32, 
 int otamd_adamw_bf16(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups, int
     n_groups, const float* clip_coef, int stochastic_rounding, unsigned long long seed, hipStream_t stream);
 
+/* replaces: same, restricted to elements [begin, end) of the flat buffers (multiples of 8; the groups and the
+   stochastic-rounding stream keep their global element indices, so chunked launches give the bits of one
+   whole-store launch).  Lets the optimizer run in parameter-range chunks on its own stream. */
+int otamd_adamw_bf16_range(void* p, const void* g, void* m, void* v, long long begin, long long end, const
+    AdamwGroup* groups, int n_groups, const float* clip_coef, int stochastic_rounding, unsigned long long seed,
+    hipStream_t stream);
+
 /* replaces: same, fp32 parameters (LoRA weights, TrainConfig.py:959) */
 int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups, int
     n_groups, const float* clip_coef, hipStream_t stream);

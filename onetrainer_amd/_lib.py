@@ -86,6 +86,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_gemm_explicit": [C.POINTER(GemmArgs), I, I, VP, LL, VP],
     "otamd_gemm_plan_tile": [C.POINTER(GemmArgs), I],
     "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
+    "otamd_adamw_bf16_range": [VP, VP, VP, VP, LL, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],
     "otamd_grad_clip_coef": [VP, I, VP, I, VP, I, F, VP, VP],
     "otamd_scale_bf16_by_device_scalar": [VP, LL, VP, VP],

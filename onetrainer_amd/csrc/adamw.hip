@@ -103,14 +103,15 @@ __device__ __forceinline__ int find_group(const AdamwGroups& G, long long e) {
 
 // flat bf16 store; n multiple of 8 (the store pads every tensor to 8 elements)
 __global__ void __launch_bounds__(256) adamw_bf16_kernel(bf16_t* __restrict__ P, const bf16_t* __restrict__ Gr,
-                                                         bf16_t* __restrict__ M, bf16_t* __restrict__ V, long long n8,
-                                                         AdamwGroups groups, const float* __restrict__ clip_coef,
-                                                         int sr, unsigned long long seed) {
+                                                         bf16_t* __restrict__ M, bf16_t* __restrict__ V, long long v0,
+                                                         long long n8, AdamwGroups groups,
+                                                         const float* __restrict__ clip_coef, int sr,
+                                                         unsigned long long seed) {
   const bool clip = clip_coef != nullptr;
   const float coef = clip ? clip_coef[0] : 1.f;
   const uint32_t k = (uint32_t)(seed ^ (seed >> 32));
   const long long stride = (long long)gridDim.x * blockDim.x;
-  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  long long i = v0 + blockIdx.x * (long long)blockDim.x + threadIdx.x;
   // software pipeline: the next granule's four loads are in flight while this one is computed
   bf8 pv, gv, mv, vv;
   if (i < n8) {
@@ -168,7 +169,7 @@ __device__ __forceinline__ void stv(bf16_t* base, long long i, bf8 x) {
 template <bool NT>
 __global__ void __launch_bounds__(1024) adamw_bf16_lut_kernel(bf16_t* __restrict__ P, const bf16_t* __restrict__ Gr,
                                                               bf16_t* __restrict__ M, bf16_t* __restrict__ V,
-                                                              long long n8, AdamwGroups groups,
+                                                              long long v0, long long n8, AdamwGroups groups,
                                                               const float* __restrict__ clip_coef, int sr,
                                                               unsigned long long seed) {
   __shared__ unsigned short lut[ADAMW_LUT_ENTRIES];
@@ -179,7 +180,7 @@ __global__ void __launch_bounds__(1024) adamw_bf16_lut_kernel(bf16_t* __restrict
   const float coef = clip ? clip_coef[0] : 1.f;
   const uint32_t k = (uint32_t)(seed ^ (seed >> 32));
   const long long stride = (long long)gridDim.x * blockDim.x;
-  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  long long i = v0 + blockIdx.x * (long long)blockDim.x + threadIdx.x;
   bf8 pv, gv, mv, vv;
   if (i < n8) {
     pv = ldv<NT>(P, i); gv = ldv<NT>(Gr, i);
@@ -316,40 +317,50 @@ static int adamw_grid(long long nvec) {
   return (int)blocks;
 }
 
-OTAMD_API int otamd_adamw_bf16(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups,
-                               int n_groups, const float* clip_coef, int stochastic_rounding,
-                               unsigned long long seed, hipStream_t stream) {
-  if (!p || !g || !m || !v || n < 0 || (n % 8) != 0 || n_groups < 1 || n_groups > ADAMW_MAX_GROUPS) return OTAMD_EINVAL;
+OTAMD_API int otamd_adamw_bf16_range(void* p, const void* g, void* m, void* v, long long begin, long long end,
+                                     const AdamwGroup* groups, int n_groups, const float* clip_coef,
+                                     int stochastic_rounding, unsigned long long seed, hipStream_t stream) {
+  if (!p || !g || !m || !v || begin < 0 || end < begin || (begin % 8) != 0 || (end % 8) != 0 || n_groups < 1 ||
+      n_groups > ADAMW_MAX_GROUPS)
+    return OTAMD_EINVAL;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return OTAMD_EINVAL;
-  if (n == 0) return OTAMD_OK;
+  if (end == begin) return OTAMD_OK;
   AdamwGroups G = {};
   for (int i = 0; i < n_groups; ++i) G.g[i] = groups[i];
   G.n = n_groups;
   // LUT kernel when the denominator constants are shared (always, for one optimizer step with common
-  // betas/eps) and the store is large enough to amortise the per-workgroup table; OTAMD_ADAMW_LUT=0
-  // forces the computed path, =1 the LUT with
-  // cached accesses, =2 the LUT with non-temporal accesses (parity tests compare them)
-  bool lut = n >= (1LL << 22);
-  for (int i = 1; i < n_groups; ++i)
-    lut = lut && G.g[i].bc2_sqrt == G.g[0].bc2_sqrt && G.g[i].eps == G.g[0].eps;
+  // betas/eps) and the range is large enough to amortise the per-workgroup table.  OTAMD_ADAMW_LUT=0
+  // forces the computed path, =1 the LUT with cached accesses, =2 the LUT with non-temporal accesses
+  // (parity tests compare them) -- never the LUT when the groups' constants differ.
+  const long long n = end - begin;
+  bool shared = true;
+  for (int i = 1; i < n_groups; ++i) shared = shared && G.g[i].bc2_sqrt == G.g[0].bc2_sqrt && G.g[i].eps == G.g[0].eps;
+  bool lut = shared && n >= (1LL << 22);
   // (measured on MI355X, 2.567 G elements: computed 7.0 ms, LUT 6.27 ms, LUT + non-temporal 6.10 ms)
   int nt = 1;
-  if (const char* e = getenv("OTAMD_ADAMW_LUT")) { lut = e[0] != '0'; nt = e[0] != '1'; }
+  if (const char* e = getenv("OTAMD_ADAMW_LUT")) { lut = shared && e[0] != '0'; nt = e[0] != '1'; }
+  const long long v0 = begin / 8, v1 = end / 8;
   if (lut) {
-    const long long nv = n / 8;
-    const int blocks = (int)std::max(1LL, std::min<long long>((nv + 1023) / 1024, 512));
+    const int blocks = (int)std::max(1LL, std::min<long long>((v1 - v0 + 1023) / 1024, 512));
     if (nt)
-      adamw_bf16_lut_kernel<true><<<blocks, 1024, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v, nv,
-                                                               G, clip_coef, stochastic_rounding, seed);
+      adamw_bf16_lut_kernel<true><<<blocks, 1024, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v, v0,
+                                                               v1, G, clip_coef, stochastic_rounding, seed);
     else
-      adamw_bf16_lut_kernel<false><<<blocks, 1024, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v, nv,
-                                                                G, clip_coef, stochastic_rounding, seed);
+      adamw_bf16_lut_kernel<false><<<blocks, 1024, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v,
+                                                                v0, v1, G, clip_coef, stochastic_rounding, seed);
   } else {
-    adamw_bf16_kernel<<<adamw_grid(n / 8), 256, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v,
-                                                             n / 8, G, clip_coef, stochastic_rounding, seed);
+    adamw_bf16_kernel<<<adamw_grid(v1 - v0), 256, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v,
+                                                               v0, v1, G, clip_coef, stochastic_rounding, seed);
   }
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
+}
+
+OTAMD_API int otamd_adamw_bf16(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups,
+                               int n_groups, const float* clip_coef, int stochastic_rounding,
+                               unsigned long long seed, hipStream_t stream) {
+  if (n < 0 || (n % 8) != 0) return OTAMD_EINVAL;
+  return otamd_adamw_bf16_range(p, g, m, v, 0, n, groups, n_groups, clip_coef, stochastic_rounding, seed, stream);
 }
 
 OTAMD_API int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups,

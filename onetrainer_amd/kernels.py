@@ -368,14 +368,17 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ksize=3, stride=1, pad=1, up
 
 # ------------------------------------------------------------------------------------------
 # optimizer
-def adamw_bf16(p, g, m, v, groups, clip_coef=None, stochastic_rounding=True, seed=0):
+def adamw_bf16(p, g, m, v, groups, clip_coef=None, stochastic_rounding=True, seed=0, begin=0, end=None):
+    """fused AdamW(+SR) over elements [begin, end) of the flat bf16 buffers (default: all)."""
     n = p.numel()
+    end = n if end is None else end
     for t in (p, g, m, v):
         _req(t.dtype == BF16 and t.is_contiguous() and t.numel() == n and _aligned(t), "adamw flat bf16 buffers")
+    _req(0 <= begin <= end <= n and begin % 8 == 0 and end % 8 == 0, "adamw range: multiples of 8 within the store")
     arr = (_lib.AdamwGroup * len(groups))(*groups)
-    check(lib().otamd_adamw_bf16(_p(p), _p(g), _p(m), _p(v), n, arr, len(groups), _p(clip_coef),
-                                 int(stochastic_rounding), seed & 0xFFFFFFFFFFFFFFFF, stream_handle()),
-          "otamd_adamw_bf16")
+    check(lib().otamd_adamw_bf16_range(_p(p), _p(g), _p(m), _p(v), begin, end, arr, len(groups), _p(clip_coef),
+                                       int(stochastic_rounding), seed & 0xFFFFFFFFFFFFFFFF, stream_handle()),
+          "otamd_adamw_bf16_range")
 
 
 def adamw_f32(p, g, m, v, groups, clip_coef=None):

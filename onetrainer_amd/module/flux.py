@@ -179,6 +179,7 @@ class FluxTransformer2DModel:
         return sum(math.prod(sh) for _, sh, _, _ in self.specs)
 
     def state_dict(self, dtype=None, grads=False):
+        self.store.wait_params()
         out = {}
         for name, *_ in self.specs:
             v = self.store.params[name].grad if grads else self.store.params[name].detach()

@@ -17,17 +17,27 @@ from . import streams as S
 
 
 class PRef:
-    """A (possibly fused) trainable tensor: value view, grad view, member names, store."""
-    __slots__ = ("store", "names", "w", "g", "params")
+    """A (possibly fused) trainable tensor: value view, grad view, member names, store.
+    Reading `w` orders the current stream after any optimizer chunk still updating it
+    (FlatParamStore.wait_params: the update of step t overlaps step t+1's forward)."""
+    __slots__ = ("store", "names", "_w", "g", "params", "_end")
 
     def __init__(self, store, names, shape=None):
         if isinstance(names, str):
             names = [names]
         self.store = store
         self.names = list(names)
-        self.w = store.view(self.names, shape)
+        self._w = store.view(self.names, shape)
         self.g = store.view(self.names, shape, grad=True)
         self.params = tuple(store.params[n] for n in self.names)
+        last = store.slots[self.names[-1]]
+        self._end = last.offset + last.numel
+
+    @property
+    def w(self):
+        if self.store.update_events is not None:
+            self.store.wait_params(self._end)
+        return self._w
 
     @property
     def trainable(self) -> bool:

@@ -59,6 +59,10 @@ class FlatParamStore:
         self._written: set[str] = set()
         self.accumulating = False          # True on micro-steps after the first of a GA window
         self.ready_hooks = []              # callables(names) -> None (DP reducer)
+        # optimizer update in flight on another stream (util/optimizer/adamw_fused.py): [(end element,
+        # event)] in layout order; a consumer of element range [.., end) waits for the events up to it
+        self.update_events: list | None = None
+        self._waited = 0
 
     # ----- views -------------------------------------------------------------------------------
     def view(self, names, shape=None, grad=False):
@@ -87,6 +91,28 @@ class FlatParamStore:
         last = self.slots[names[-1]]
         return first.offset, last.offset + last.numel
 
+    # ----- asynchronous optimizer updates ------------------------------------------------------------
+    def set_update_events(self, events):
+        self.update_events = events or None
+        self._waited = 0
+
+    def wait_params(self, end: int | None = None):
+        """make the current stream wait for the optimizer chunks covering elements [0, end) (all when
+        end is None).  Forward order = layout order, so a forward that reaches layer L waits only for the
+        chunks up to L's weights; the rest of the update keeps running beside it."""
+        ev = self.update_events
+        if ev is None:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        while self._waited < len(ev):
+            e_end, e = ev[self._waited]
+            cur.wait_event(e)
+            self._waited += 1
+            if end is not None and e_end >= end:
+                break
+        if self._waited >= len(ev):
+            self.update_events = None
+
     # ----- gradient bookkeeping -----------------------------------------------------------------
     def accumulate_into(self, names) -> bool:
         """True if a backward kernel must add into the grad view (GA window), else overwrite."""
@@ -98,6 +124,7 @@ class FlatParamStore:
             h(names)
 
     def begin_backward(self):
+        self.wait_params()   # backward overwrites the gradients the optimizer chunks read
         self._written.clear()
 
     def finish_backward(self):

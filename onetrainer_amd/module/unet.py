@@ -247,6 +247,7 @@ class UNet2DConditionModel:
         return sum(math.prod(sh) for _, sh, _, _ in self.specs)
 
     def state_dict(self, dtype=None, grads=False):
+        self.store.wait_params()
         """diffusers-layout state dict (NCHW conv weights, unpadded); grads=True exports gradients."""
         out = {}
         for name, shape, kind, _ in self.specs:

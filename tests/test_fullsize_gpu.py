@@ -141,6 +141,7 @@ def _steps(tr, batches, store):
         losses.append(tr.train_step(b).float().item())
         if i == 0:
             assert bool(torch.isfinite(store.grad).all().item()), "non-finite gradients"
+        store.wait_params()                  # the optimizer update runs on its own stream (adamw_fused.py)
         snaps.append(store.data.clone() if store.numel < 3_000_000_000 else None)
     return losses, snaps
 

@@ -119,3 +119,30 @@ def test_adamw_lut_matches_computed_path(dev, sr, clip, monkeypatch):
     for o in outs[1:]:
         for a, b, name in zip(outs[0], o, "pmv"):
             assert torch.equal(a, b), (name, int((a != b).sum()))
+
+
+def test_overlapped_chunked_adamw_matches_single_launch(dev, monkeypatch):
+    """util/optimizer/adamw_fused.py overlap: 16 range chunks on the optimizer stream (events per chunk,
+    FlatParamStore.wait_params) give the bits of the one-launch update, SR on, clip on."""
+    shapes = [(f"t{i}", (4_500_000 + 8 * i,)) for i in range(16)]       # 72 M elements >= the 64 M threshold
+    runs = []
+    for overlap in ("0", "1"):
+        monkeypatch.setenv("OTAMD_OPT_OVERLAP", overlap)
+        torch.manual_seed(0)
+        st = FlatParamStore([(n, s, "g") for n, s in shapes], torch.bfloat16, dev)
+        st.data.copy_((torch.randn(st.numel, device=dev) * 0.05).to(torch.bfloat16))
+        opt = FusedAdamW(st, [{"params": [st.params[n] for n, _ in shapes]}], lr=1e-3, stochastic_rounding=True,
+                         seed=7)
+        assert opt.overlap == (overlap == "1")
+        for step in range(2):
+            g = torch.Generator(device=dev).manual_seed(100 + step)
+            st.grad.copy_((torch.randn(st.numel, device=dev, generator=g) * 0.5).to(torch.bfloat16))
+            opt.clip_grad_norm_(1.0)
+            opt.step()
+            if overlap == "1":
+                assert st.update_events is not None and len(st.update_events) == len(opt._opt_chunks) >= 8
+        st.wait_params()
+        torch.cuda.synchronize()
+        runs.append((st.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
