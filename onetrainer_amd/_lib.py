@@ -85,6 +85,8 @@ SIGNATURES: dict[str, list] = {
     "otamd_gemm_plan": [C.POINTER(GemmArgs), I, C.POINTER(C.c_int)],
     "otamd_gemm_explicit": [C.POINTER(GemmArgs), I, I, VP, LL, VP],
     "otamd_gemm_plan_tile": [C.POINTER(GemmArgs), I],
+    "otamd_gemm_sk_errors": [],
+    "otamd_gemm_coop_reserve": [VP],
     "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_bf16_range": [VP, VP, VP, VP, LL, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],

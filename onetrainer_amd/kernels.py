@@ -9,6 +9,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import os
+
 import torch
 
 from . import _lib
@@ -99,7 +101,7 @@ def _tune(a: GemmArgs, device) -> tuple:
         seen.add(se)
         ws_bytes = se * a.M * a.N * 4 if se > 1 else 0
         ws = workspace(ws_bytes, device) if ws_bytes else None
-        for t in _TILES:
+        for t in _TILES:   # (not 5, coop split-K: slower on every measured shape, gemm.hip sk_enabled)
             if v2_only and t < 0:
                 continue
             rc = lib().otamd_gemm_explicit(C.byref(b), t, se, _p(ws), ws_bytes, stream_handle())
@@ -117,9 +119,34 @@ def _tune(a: GemmArgs, device) -> tuple:
     return best
 
 
+def _plan_overrides() -> dict:
+    """OTAMD_GEMM_PLAN="am,bm,M,N,K:tile:splits;..." pins the (tile, split-K) of listed GEMM shapes
+    (A/B measurements of planner changes inside the real step)."""
+    env = os.environ.get("OTAMD_GEMM_PLAN", "")
+    out = {}
+    for item in filter(None, env.split(";")):
+        key, tile, sp = item.split(":")
+        out[tuple(int(x) for x in key.split(","))] = (int(tile), int(sp))
+    return out
+
+
+_PLAN_OVERRIDES = None
+
+
 def _gemm(a: GemmArgs, splits: int, device) -> None:
     """splits = 0: the library plans tile shape and split-K (otamd_gemm_plan), or the autotuner's
     cached plan when set_gemm_autotune(True)."""
+    global _PLAN_OVERRIDES
+    if _PLAN_OVERRIDES is None:
+        _PLAN_OVERRIDES = _plan_overrides()
+    if splits == 0 and _PLAN_OVERRIDES:
+        ov = _PLAN_OVERRIDES.get((a.amode, a.bmode, a.M, a.N, a.K))
+        if ov is not None:
+            t, s = ov
+            ws_bytes = s * a.M * a.N * 4 if s > 1 else 0
+            ws = workspace(ws_bytes, device) if ws_bytes else None
+            check(lib().otamd_gemm_explicit(C.byref(a), t, s, _p(ws), ws_bytes, stream_handle()), "otamd_gemm_explicit")
+            return
     if splits == 0 and _gemm_forced_splits:
         splits = _gemm_forced_splits
     if splits == 0 and _TUNE["on"]:

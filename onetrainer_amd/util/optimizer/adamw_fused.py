@@ -9,14 +9,15 @@ zero_grad(set_to_none), state_dict()/load_state_dict() (torch AdamW layout: per-
 'exp_avg', 'exp_avg_sq'), step_parameter(p, group, i).  The arithmetic is one launch over the
 flat store (csrc/adamw.hip) instead of ~8 torch ops per tensor.
 
-Overlap (bf16 stores of >= 64 M elements, OTAMD_OPT_OVERLAP=0 disables): step() runs the update on
+Overlap (opt-in, OTAMD_OPT_OVERLAP=1; bf16 stores of >= 64 M elements): step() runs the update on
 its own stream in 16 parameter-range chunks (layout = forward order) and records an event per chunk
 in the store; the next forward's kernels wait only for the chunk holding their weights
 (FlatParamStore.wait_params via PRef.w), so the 36 GB optimizer pass (SDXL: ~6 ms of HBM time)
 runs beside the compute-bound forward GEMMs instead of in front of them.  Chunked launches give the
 bits of one whole-store launch (global element indices for groups and stochastic rounding).
 Readers of the parameters outside the train step call store.wait_params() (state_dict, savers and
-backups do).
+backups do).  Measured on the SDXL step (MI355X): no gain (151.1 vs 150.6 ms p50) -- a 256x256 GEMM
+workgroup takes a whole CU's register file, so the update only time-slices CUs with the forward.
 """
 from __future__ import annotations
 
@@ -72,7 +73,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.clip_out = torch.zeros(2, dtype=torch.float32, device=store.device)   # [coef, total norm]
         # overlapped update: chunk boundaries on tensor boundaries, ~numel / 16 each
         self.overlap = (store.device.type == "cuda" and store.dtype == torch.bfloat16 and store.numel >= (1 << 26)
-                        and os.environ.get("OTAMD_OPT_OVERLAP", "1") != "0")
+                        and os.environ.get("OTAMD_OPT_OVERLAP", "0") == "1")
         self._opt_chunks = []
         if self.overlap:
             target = store.numel // 16
@@ -90,6 +91,7 @@ class FusedAdamW(torch.optim.Optimizer):
     # --- clip_grad_norm_ (GenericTrainer.py:712-713) ----------------------------------------------
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
         """computes the clip coefficient on device; it is applied inside the next step()."""
+        self.store.wait_params()   # the previous (overlapped) update still reads grads / clip_out
         K.grad_clip_coef(self.store.grad, self._chunks, self._n_chunks, self._tensor_sq, len(self.store.order),
                          max_norm, self.clip_out)
         self._pending_clip = True

@@ -135,6 +135,7 @@ def test_overlapped_chunked_adamw_matches_single_launch(dev, monkeypatch):
                          seed=7)
         assert opt.overlap == (overlap == "1")
         for step in range(2):
+            st.wait_params()      # what store.begin_backward does before gradients are rewritten
             g = torch.Generator(device=dev).manual_seed(100 + step)
             st.grad.copy_((torch.randn(st.numel, device=dev, generator=g) * 0.5).to(torch.bfloat16))
             opt.clip_grad_norm_(1.0)
