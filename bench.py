@@ -34,9 +34,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(res=512, steps=1, sd15=False):
-    """Oracle (CPU fp32 restatement of the reference step: diffusers UNet + DDPM noise + MSE +
-    clip + torch AdamW) timed on this host's cores, SDXL at `res`^2, batch 1."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(res=512, sd15=False, warmup=1, timed=3):
+    """the oracle (test infrastructure: the CPU fp32 restatement of the reference
+    step -- diffusers-architecture UNet fwd+bwd, DDPM noise + timesteps seeded per step, MSE,
+    clip_grad_norm 1.0, torch AdamW) on this host's cores at batch 1: `warmup` untimed steps, then
+    `timed` steps.  Returns (step seconds list, threads)."""
     from oracle import unet as OU
     from oracle import diffusion as OD
     threads = len(os.sched_getaffinity(0))
@@ -44,7 +57,6 @@ def cpu_baseline(res=512, steps=1, sd15=False):
     torch.set_num_threads(threads)
     cfg = OU.sd15_config() if sd15 else OU.sdxl_config()
     torch.manual_seed(0)
-    t0 = time.time()
     with torch.device("meta"):
         m = OU.UNet2DConditionModel(cfg)
     m = m.to_empty(device="cpu")
@@ -54,11 +66,10 @@ def cpu_baseline(res=512, steps=1, sd15=False):
     opt = torch.optim.AdamW(m.parameters(), lr=3e-6, weight_decay=1e-2, foreach=True)
     betas = OD.scaled_linear_betas()
     h = res // 8
-    x0 = torch.randn(1, 4, h, h)
+    x0 = torch.randn(1, 4, h, h)   # the scaled latent: N(0,1)/scaling_factor cached, times scaling_factor
     ehs = torch.randn(1, 77, cfg.cross_attention_dim)
     te = None if sd15 else torch.randn(1, 1280)
     tid = None if sd15 else torch.tensor([[float(res), float(res), 0., 0., float(res), float(res)]])
-    build_s = time.time() - t0
 
     def step(i):
         g = torch.Generator().manual_seed(i)
@@ -72,12 +83,17 @@ def cpu_baseline(res=512, steps=1, sd15=False):
         opt.step()
         opt.zero_grad(set_to_none=True)
 
-    t0 = time.time()
-    for i in range(steps):
+    times = []
+    for i in range(warmup + timed):
+        t0 = time.perf_counter()
         step(i)
-    dt = (time.time() - t0) / steps
+        dt = time.perf_counter() - t0
+        log(f"[bench] cpu baseline {'SD1.5' if sd15 else 'SDXL'} {res}^2 step {i} {dt:.2f}s"
+            f"{' (warm-up)' if i < warmup else ''}")
+        if i >= warmup:
+            times.append(dt)
     del m, opt
-    return dt, threads, build_s
+    return times, threads
 
 
 def gemm_roofline(tr, batch):
@@ -155,7 +171,6 @@ def main():
                          "(SDXL LoRA r32, aspect-ratio buckets drawn per step, b=4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true", help="skip the VAE-encode (latent caching) side measurement")
-    ap.add_argument("--cpu-res", type=int, default=512)
     ap.add_argument("--autotune", action="store_true",
                     help="time (tile, split-K) candidates per GEMM signature in warm-up instead of the analytic plan "
                          "(measured: no gain on the SDXL step -- isolated warm-cache timings do not transfer)")
@@ -342,16 +357,28 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not flux and not sdxl_lora:
         del tr
         torch.cuda.empty_cache()
-        log("[bench] cpu baseline (oracle, fp32) ...")
         try:
-            dt, threads, build_s = cpu_baseline(args.cpu_res, 1, sd15)
-            cpu_tf = 3.0 * flops_per_image(ucfg, args.cpu_res // 8, args.cpu_res // 8) / 1e12
-            eq = (1.0 / dt) * cpu_tf / train_tf_img        # images/s at the bench resolution, by FLOP ratio
-            out["cpu_baseline"] = {"value": round(eq, 5), "unit": "images/s", "cores": threads, "kind": "port",
-                                   "sample": f"1 step of the oracle (CPU fp32 restatement: UNet fwd+bwd, DDPM noise, "
-                                             f"MSE, clip, torch AdamW) at {args.model} {args.cpu_res}^2 b=1 took {dt:.2f}s; "
-                                             f"value scaled to {args.res}^2 by the FLOP ratio "
-                                             f"({cpu_tf:.2f}/{train_tf_img:.2f} TFLOP)"}
+            # C1 (SD 1.5 preset, 512^2, b=1): 1 warm-up + 3 timed, p50; then the bench workload's own
+            # network at its resolution, b=1 (SDXL 1024^2: 1 warm-up + 1 timed) -> `value`
+            c1, threads = cpu_baseline(512, sd15=True, warmup=1, timed=3)
+            c1_p50 = sorted(c1)[len(c1) // 2]
+            if sd15 and args.res == 512:
+                big, big_p50 = c1, c1_p50
+            else:
+                big, _ = cpu_baseline(args.res, sd15=sd15, warmup=1, timed=1)
+                big_p50 = sorted(big)[len(big) // 2]
+            out["cpu_baseline"] = {
+                "value": round(1.0 / big_p50, 5), "unit": "images/s", "cores": threads, "kind": "port",
+                "cpu_model": cpu_model(), "threads": threads,
+                "sample": (f"oracle (CPU fp32 restatement of the reference step: UNet fwd+bwd, DDPM noise, MSE, clip, "
+                           f"torch AdamW) on {threads} threads of {cpu_model()}: "
+                           f"{'SD 1.5' if sd15 else 'SDXL 1.0'} {args.res}^2 b=1, 1 warm-up + {len(big)} timed step(s), "
+                           f"p50 {big_p50:.2f} s -> value; C1 SD 1.5 512^2 b=1 1 warm-up + 3 timed p50 "
+                           f"{c1_p50:.2f} s ({1.0 / c1_p50:.4f} images/s)"),
+                "c1_sd15_512_b1": {"step_s": [round(x, 3) for x in c1], "p50_s": round(c1_p50, 3),
+                                   "images_per_s": round(1.0 / c1_p50, 5)},
+                "workload_b1": {"step_s": [round(x, 3) for x in big], "p50_s": round(big_p50, 3)},
+            }
         except Exception as e:   # the baseline must not sink the GPU measurement
             out["cpu_baseline"] = {"value": None, "unit": "images/s", "cores": None, "kind": "port",
                                    "sample": f"failed: {e!r}"}

@@ -99,15 +99,8 @@ long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out);
 int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                         hipStream_t stream);
 
-/* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves,
-   4 128x128/8 waves, 5 stream-K (256x256 tiles, one persistent workgroup per CU; otamd_gemm_explicit's splits = workgroups) */
+/* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves */
 int otamd_gemm_plan_tile(const GemmArgs* in, int splits);
-
-/* replaces: (graph capture support) allocate a stream's coop split-K state before capturing on it */
-int otamd_gemm_coop_reserve(hipStream_t stream);
-
-/* replaces: (diagnostic) coop split-K launches whose partial hand-off timed out since the last call (synchronises; expected 0) */
-int otamd_gemm_sk_errors(void);
 
 /* replaces: ABI check */
 int otamd_gemm_args_size(void);

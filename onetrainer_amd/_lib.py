@@ -33,8 +33,7 @@ class GemmArgs(C.Structure):
                 ("A2", C.c_void_p), ("lda2", C.c_longlong), ("B2", C.c_void_p), ("ldb2", C.c_longlong),
                 ("K1", C.c_int), ("K2", C.c_int),
                 ("batch", C.c_int), ("bdiv", C.c_int), ("sa0", C.c_longlong), ("sa1", C.c_longlong),
-                ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong),
-                ("tile_ctr", C.c_void_p)]
+                ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong)]
 
 
 class AdamwGroup(C.Structure):
@@ -85,8 +84,6 @@ SIGNATURES: dict[str, list] = {
     "otamd_gemm_plan": [C.POINTER(GemmArgs), I, C.POINTER(C.c_int)],
     "otamd_gemm_explicit": [C.POINTER(GemmArgs), I, I, VP, LL, VP],
     "otamd_gemm_plan_tile": [C.POINTER(GemmArgs), I],
-    "otamd_gemm_sk_errors": [],
-    "otamd_gemm_coop_reserve": [VP],
     "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_bf16_range": [VP, VP, VP, VP, LL, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],
@@ -157,11 +154,17 @@ def lib():
     """Load libotamd.so once.  Raises if it is absent: there is no fallback path."""
     global _lib
     if _lib is None:
-        if not LIB_PATH.exists():
-            raise RuntimeError(f"onetrainer_amd HIP library not built: {LIB_PATH} missing "
+        path = LIB_PATH
+        alt = os.environ.get("OTAMD_LIB_ALT")   # A/B measurements: another build of this library (tools/ab_lib.sh)
+        if alt:
+            path = LIB_PATH.with_name(f"libotamd_{alt}.so")
+        if not path.exists():
+            raise RuntimeError(f"onetrainer_amd HIP library not built: {path} missing "
                                "(run `python -m onetrainer_amd.build`); there is no CPU fallback")
-        L = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+        L = C.CDLL(str(path), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
         for name, args in SIGNATURES.items():
+            if alt and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_plan", "_part_floats")) else C.c_int

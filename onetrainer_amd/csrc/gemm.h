@@ -40,10 +40,6 @@ struct GemmArgs {
   // [B, N, H*D] activation are bdiv = H, s0 = batch stride, s1 = D.  batch <= 1: unbatched.
   int batch, bdiv;
   long long sa0, sa1, sb0, sb1, sc0, sc1;
-  // split-K arrival counters, one per output tile (set by the launcher, never by callers): the
-  // last workgroup of a tile to store its partial sums the slabs itself (no reduce launch);
-  // zero between launches (the last arriver resets its counter), per stream
-  unsigned* tile_ctr;
 };
 
 __device__ __forceinline__ void gemm_batch_offset(GemmArgs& a) {
@@ -70,40 +66,12 @@ __device__ __forceinline__ bool gemm_wide_ok(const GemmArgs& a) {
   return (al & 15) == 0 && (a.ldc % 8) == 0 && (!a.rowvec || (a.ldv % 8) == 0) && (!a.residual || (a.ldr % 8) == 0);
 }
 
-// Split-K slab access for the in-kernel fix-up: sc1 (device-coherent) buffer stores / loads go
-// past the XCD-private L2, so partials written by workgroups on other XCDs are visible to the
-// last arriver after an s_waitcnt + counter atomic -- no agent-scope fences (their L2
-// write-back + invalidate stalled every concurrently running kernel: step 150 -> 204 ms).
-// Offsets are byte offsets into the slab (< 2^31, checked by the launcher).
-typedef unsigned slab_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const GemmArgs& args) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)args.slab, (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ void slab_store_coh(const GemmArgs& args, long long e, float a, float b, float c, float d) {
-  slab_u4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, slab_rsrc(args), (int)(e * 4), 0, 16);
-}
-template <bool COH>
-__device__ __forceinline__ float4 slab_load(const GemmArgs& args, long long e) {
-  if constexpr (COH) {
-    const slab_u4 v = __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc(args), (int)(e * 4), 0, 16);
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-  } else {
-    return *reinterpret_cast<const float4*>(args.slab + e);
-  }
-}
-
 // epilogue for 8 consecutive output columns n..n+7 of row m: same math as gemm_store4, 16-byte
 // loads / stores (half the store instructions of the 4-column form; the tail is issue-bound)
 __device__ __forceinline__ void gemm_store8(const GemmArgs& args, int m, int n, float (&v)[8], int split,
                                             bool use_slab) {
   if (use_slab) {
     const long long e = ((long long)split * args.M + m) * args.N + n;
-    if (args.tile_ctr) {
-      slab_store_coh(args, e, v[0], v[1], v[2], v[3]);
-      slab_store_coh(args, e + 4, v[4], v[5], v[6], v[7]);
-      return;
-    }
     float* dst = args.slab + e;
     reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
     reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
@@ -139,10 +107,6 @@ __device__ __forceinline__ void gemm_store4(const GemmArgs& args, int m, int n, 
                                             bool use_slab) {
   if (use_slab) {
     const long long e = ((long long)split * args.M + m) * args.N + n;
-    if (args.tile_ctr) {
-      slab_store_coh(args, e, v[0], v[1], v[2], v[3]);
-      return;
-    }
     *reinterpret_cast<float4*>(args.slab + e) = make_float4(v[0], v[1], v[2], v[3]);
     return;
   }
@@ -206,18 +170,21 @@ __device__ __forceinline__ int kimg_off(int row, int chunk) { return row * 128 +
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
 // alpha * sum_s slab[s] (+bias, +rowvec, +residual) (+C if accumulate) for V consecutive columns
-// n.. of row m: the split-K combine, shared by splitk_reduce_kernel and the GEMM's in-kernel
-// last-arriver fix-up so both give the same bits (splits summed in index order).
-template <int V, bool COH = false>
+// n.. of row m: the split-K combine of splitk_reduce_kernel (splits summed in index order).
+__device__ __forceinline__ float4 slab_load(const GemmArgs& args, long long e) {
+  return *reinterpret_cast<const float4*>(args.slab + e);
+}
+
+template <int V>
 __device__ __forceinline__ void splitk_combine(const GemmArgs& args, unsigned m, unsigned n, int splits) {
   const long long MN = (long long)args.M * args.N;
   const long long e = (long long)m * args.N + n;
   float v[V];
   {
-    const float4 t = slab_load<COH>(args, e);
+    const float4 t = slab_load(args, e);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
     if constexpr (V == 8) {
-      const float4 u = slab_load<COH>(args, e + 4);
+      const float4 u = slab_load(args, e + 4);
       v[4] = u.x; v[5] = u.y; v[6] = u.z; v[7] = u.w;
     }
   }
@@ -227,7 +194,7 @@ __device__ __forceinline__ void splitk_combine(const GemmArgs& args, unsigned m,
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int h = 0; h < V / 4; ++h) t[q][h] = slab_load<COH>(args, (z + q) * MN + e + 4 * h);
+      for (int h = 0; h < V / 4; ++h) t[q][h] = slab_load(args, (z + q) * MN + e + 4 * h);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -238,7 +205,7 @@ __device__ __forceinline__ void splitk_combine(const GemmArgs& args, unsigned m,
   for (; z < splits; ++z)
 #pragma unroll
     for (int h = 0; h < V / 4; ++h) {
-      const float4 t = slab_load<COH>(args, z * MN + e + 4 * h);
+      const float4 t = slab_load(args, z * MN + e + 4 * h);
       v[4 * h] += t.x; v[4 * h + 1] += t.y; v[4 * h + 2] += t.z; v[4 * h + 3] += t.w;
     }
 #pragma unroll

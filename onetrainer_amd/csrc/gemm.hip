@@ -22,9 +22,7 @@
 
 #include <stdlib.h>
 
-#include <algorithm>
 #include <mutex>
-#include <unordered_map>
 #include <string.h>
 
 #define BM 128
@@ -317,10 +315,6 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream);  
 // (tile MACs / relative tile throughput + fixed prologue/epilogue) + split-K slab reduce traffic.
 // Relative throughputs are from tools/gemm_bench.py on MI355X.  OTAMD_GEMM_TILE forces the tile.
 struct GemmPlan { int tile, splits; };
-enum { TILE_SK = 5 };   // stream-K (gemm2.hip): 256x256 tiles, one persistent workgroup per CU
-
-int gemm2_sk_launch(const GemmArgs& a, int P, hipStream_t stream);   // gemm2.hip
-int gemm2_cu_count();
 
 static int forced_tile() {
   static int forced = -2;
@@ -354,46 +348,11 @@ static bool no_tile4() {   // OTAMD_GEMM_NO_T4=1: plan without the 128x128 tile 
   return v;
 }
 
-// OTAMD_GEMM_SK=1: coop split-K (gemm2.hip) as a candidate of the automatic plan.  OPT-IN: measured
-// on MI355X it loses to the tile plans on every SDXL shape it would take (4096x1280x1280: coop
-// 56-60 us vs 23-26 us for the 128x128 tile, tools/gemm_tiles.py, profiles/r2_coop_tiles.jsonl)
-// -- the partial hand-off between the workgroups of a tile goes through sc1 (device-coherent)
-// traffic at one CU's bandwidth and costs ~40 us, more than the wave quantisation it removes; and
-// the SDXL step with it on the main and wgrad streams ran 2.4 s/step (two co-scheduled grids
-// whose groups wait on each other's CUs until the bounded spin gives up).
-static bool sk_enabled() {
-  static const int v = [] {
-    const char* e = getenv("OTAMD_GEMM_SK");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v == 1;
-}
-
-// coop split-K time (gemm2.hip): the busiest workgroup runs ceil(nkt / floor(P/T)) 64-deep K-steps
-// of a 256x256 tile; then the tile's partials go through L2 (each workgroup writes its fp32 tile
-// and reads 1/s of every peer's: ~2 x 256 KB at one CU's L2 bandwidth)
-static double sk_cost(int M, int N, int K, double cu_flops) {
-  const int cus = gemm2_cu_count();
-  if (cus <= 0) return 1e300;
-  const long long T = (long long)((M + 255) / 256) * ((N + 255) / 256), nkt = (K + 63) / 64;
-  if (T > cus) return 1e300;
-  const long long P = std::min<long long>(cus, T * nkt);   // gemm2_sk_launch's workgroup count
-  const long long s0 = P / T, smax = (P + T - 1) / T;
-  if (smax > 1 && smax * M * N * 4LL >= (1LL << 31)) return 1e300;
-  const long long per = (nkt + s0 - 1) / s0;
-  const double kstep = 2.0 * 256 * 256 * 64 / cu_flops;
-  return per * kstep + 2.5e-6 + (smax > 1 ? 3.0e-6 : 0.0);
-}
-
-static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = false, bool sk_ok = false) {
+static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = false) {
   const double cu_flops = 1.1e15 / 256.0;    // effective per-CU rate of the 256x256 tile
   const int ft = forced_tile();
   GemmPlan best = {-1, 1};
   double best_t = 1e300;
-  if (sk_ok && ft == -3 && sk_enabled()) {
-    best_t = sk_cost(M, N, K, cu_flops);
-    if (best_t < 1e300) best = {TILE_SK, 1};
-  }
   for (const TileCand& c : kTiles) {
     if (ft != -3 && c.tile != ft) continue;
     if (v2_only && c.tile < 0) continue;
@@ -420,9 +379,6 @@ static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = fa
   return best;
 }
 
-// forms the stream-K kernel takes (the v2 forms; unbatched)
-static bool sk_form(const GemmArgs& a) { return a.batch <= 1; }
-
 // C-ABI.  Preconditions (checked, OTAMD_EINVAL otherwise): M,N,K > 0; N % 4 == 0; K-mode
 // operands need K % 8 == 0, MN-mode operands MN % 8 == 0; leading dims multiples of 8
 // elements; base pointers 16-byte aligned; conv gathers need SC % 8 == 0.
@@ -432,7 +388,7 @@ OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -1;
   int s = splits;
   if (in->batch > 1) s = 1;
-  if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT || in->A2 != nullptr, sk_form(*in)).splits;
+  if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT || in->A2 != nullptr).splits;
   if (splits_out) *splits_out = s;
   return s > 1 ? (long long)s * in->M * in->N * 4 : 0;
 }
@@ -444,9 +400,8 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
 OTAMD_API int otamd_gemm_plan_tile(const GemmArgs* in, int splits) {
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -9;
   const bool v2_only = in->bmode == OPM_CONV_WT || in->A2 != nullptr;
-  GemmPlan plan = plan_gemm(in->M, in->N, in->K, splits > 0 ? splits : 32, v2_only, sk_form(*in));
-  if (splits > 0) plan = plan_gemm(in->M, in->N, in->K, 1, v2_only, splits == 1 && sk_form(*in)), plan.splits = splits;
-  if (plan.tile == TILE_SK) return TILE_SK;
+  GemmPlan plan = plan_gemm(in->M, in->N, in->K, splits > 0 ? splits : 32, v2_only);
+  if (splits > 0) plan = plan_gemm(in->M, in->N, in->K, 1, v2_only), plan.splits = splits;
   const long long kps = ((long long)(in->K + plan.splits - 1) / plan.splits + BK - 1) / BK * BK;
   return resolve_tile(*in, (int)((in->K + kps - 1) / kps), plan, v2_only);
 }
@@ -470,42 +425,9 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
   return tile;
 }
 
-// Split-K arrival counters for the in-kernel fix-up (gemm2.hip), one array per stream: kernels
-// of one stream run in order and each last arriver re-zeroes its counter, so an array is all
-// zero whenever a launch starts.  Allocated (and zeroed) at the stream's first split-K launch.
-// OPT-IN (OTAMD_SPLITK_FIXUP=1): measured on the SDXL step it is slower than the reduce kernel
-// (150 -> 165 ms/step): each tile's last arriver sums 2-7 fp32 partials on ONE CU, a serial tail
-// per tile, while splitk_reduce_kernel spreads the same bytes over the whole chip.  Kept, with its
-// parity test, as the base for a fix-up spread over all split workgroups of a tile.
-#define SPLITK_MAX_TILES 65536
-static unsigned* splitk_counters(hipStream_t stream, long long tiles) {
-  if (tiles > SPLITK_MAX_TILES) return nullptr;
-  const char* e = getenv("OTAMD_SPLITK_FIXUP");
-  if (!e || e[0] != '1') return nullptr;
-  static std::mutex mu;
-  static std::unordered_map<hipStream_t, unsigned*> ctrs;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = ctrs.find(stream);
-  if (it != ctrs.end()) return it->second;
-  // no allocation while the stream is being captured into a graph: that launch keeps the reduce kernel
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  unsigned* p = nullptr;
-  if (hipMalloc(&p, SPLITK_MAX_TILES * sizeof(unsigned)) != hipSuccess) return nullptr;
-  if (hipMemset(p, 0, SPLITK_MAX_TILES * sizeof(unsigned)) != hipSuccess) { (void)hipFree(p); return nullptr; }
-  ctrs.emplace(stream, p);
-  return p;
-}
-
-// workgroups along grid.x of a v2 launch (gemm2_launch's tile sizes)
-static long long tile_count(const GemmArgs& a, int tile) {
-  const int bm = (tile == 2 || tile == 4) ? 128 : 256, bn = (tile == 1 || tile == 4) ? 128 : 256;
-  return (long long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
-}
-
 // force_tile: -9 = planned; otherwise the tile code (-1 v1, 0..3 v2) and splits >= 1 as given
 static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* workspace, long long ws_bytes,
-                     hipStream_t stream, int sk_p = 0) {
+                     hipStream_t stream) {
   if (!in) return OTAMD_EINVAL;
   GemmArgs a = *in;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
@@ -523,9 +445,8 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
     if ((a.sa0 | a.sa1 | a.sb0 | a.sb1) % 8 || (a.sc0 | a.sc1) % 4) return OTAMD_EINVAL;
     splits = 1;
   }
-  const bool sk_ok = force_tile == -9 && sk_form(a);
-  GemmPlan plan = plan_gemm(a.M, a.N, a.K, splits > 0 ? splits : 32, v2_only, sk_ok);
-  if (splits > 0) plan = plan_gemm(a.M, a.N, a.K, 1, v2_only, sk_ok && splits == 1), plan.splits = splits;
+  GemmPlan plan = plan_gemm(a.M, a.N, a.K, splits > 0 ? splits : 32, v2_only);
+  if (splits > 0) plan = plan_gemm(a.M, a.N, a.K, 1, v2_only), plan.splits = splits;
   splits = plan.splits;
   if (!a.A || !a.B || !a.C || !aligned16(a.A) || !aligned16(a.B)) return OTAMD_EINVAL;
   gemm_fn fn = pick(a.amode, a.bmode);
@@ -548,25 +469,11 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   } else {
     a.slab = nullptr;
   }
-  if (force_tile == TILE_SK || plan.tile == TILE_SK) {
-    a.slab = nullptr;
-    a.tile_ctr = nullptr;
-    const int rc = gemm2_sk_launch(a, force_tile == TILE_SK ? sk_p : 0, stream);
-    if (rc == OTAMD_OK || rc == OTAMD_ELAUNCH || force_tile == TILE_SK) return rc;
-    plan = plan_gemm(a.M, a.N, a.K, 1, v2_only, false);   // not here (graph capture / extents): tile plan
-  }
   int tile = force_tile == -9 ? resolve_tile(a, splits, plan, v2_only) : force_tile;
   if (v2_only && tile < 0) return OTAMD_EUNSUPPORTED;
   int rc = OTAMD_EUNSUPPORTED;
-  a.tile_ctr = nullptr;
-  if (tile >= 0) {
-    if (splits > 1 && (long long)splits * a.M * a.N * 4 < (1LL << 31))   // sc1 slab offsets are 31-bit
-      a.tile_ctr = splitk_counters(stream, tile_count(a, tile));
-    rc = gemm2_launch(a, tile, splits, stream);
-  }
+  if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
-  const bool fixed_up = rc == OTAMD_OK && a.tile_ctr != nullptr;
-  a.tile_ctr = nullptr;
   if (rc != OTAMD_OK) {
     if (!fn || a.A2) return rc;   // v1 has no conv-weight B and no second K segment
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -574,7 +481,7 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);
     OTAMD_CHECK_LAUNCH();
   }
-  if (splits > 1 && !fixed_up) {
+  if (splits > 1) {
     // 8-wide needs 16-byte aligned rows of C (bf16: ldc % 8, fp32 handled element-wise)
     const bool v8 = (a.N % 8) == 0 && (a.ldc % 8) == 0 && ((uintptr_t)a.C & 15) == 0;
     const long long nv = (long long)a.M * a.N / (v8 ? 8 : 4);
@@ -593,12 +500,10 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
 
 // explicit plan (the autotuner's candidates and its cached choice): tile -1 = v1 128x128, 0 = 256x256,
 // 1 = 256x128, 2 = 128x256, 3 = 256x256 (4 waves), 4 = 128x128 (8 waves, 2 workgroups per CU);
-// splits >= 1 (rounded to whole 64-deep K steps).  tile 5 = stream-K: `splits` is then the number of
-// persistent workgroups P (1 = one per CU), no workspace.
+// splits >= 1 (rounded to whole 64-deep K steps)
 OTAMD_API int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                                   hipStream_t stream) {
-  if (tile < -1 || tile > TILE_SK || splits < 1) return OTAMD_EINVAL;
-  if (tile == TILE_SK) return gemm_impl(in, 1, TILE_SK, nullptr, 0, stream, splits > 1 ? splits : 0);
+  if (tile < -1 || tile > 4 || splits < 1) return OTAMD_EINVAL;
   return gemm_impl(in, splits, tile, workspace, ws_bytes, stream);
 }
 

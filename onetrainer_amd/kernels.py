@@ -101,7 +101,7 @@ def _tune(a: GemmArgs, device) -> tuple:
         seen.add(se)
         ws_bytes = se * a.M * a.N * 4 if se > 1 else 0
         ws = workspace(ws_bytes, device) if ws_bytes else None
-        for t in _TILES:   # (not 5, coop split-K: slower on every measured shape, gemm.hip sk_enabled)
+        for t in _TILES:
             if v2_only and t < 0:
                 continue
             rc = lib().otamd_gemm_explicit(C.byref(b), t, se, _p(ws), ws_bytes, stream_handle())

@@ -43,7 +43,6 @@ class StepGraphs:
         self.entries: dict = {}
         self.seen: dict = {}
         self.pool = None
-        self.stream = None     # capture stream (its coop GEMM state is allocated before capturing)
 
     @staticmethod
     def enabled_for(trainer) -> bool:
@@ -90,14 +89,9 @@ class StepGraphs:
         torch.cuda.synchronize()
         torch.cuda.empty_cache()   # the eager steps' cached blocks; the graph gets its own pool
         g = torch.cuda.CUDAGraph()
-        if self.stream is None:
-            from onetrainer_amd import kernels as K
-            self.stream = torch.cuda.Stream()
-            K.check(K.lib().otamd_gemm_coop_reserve(self.stream.cuda_stream), "otamd_gemm_coop_reserve")
-            torch.cuda.synchronize()
         setup.graph_inputs = (e.noise, e.timestep)
         try:
-            with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+            with torch.cuda.graph(g, pool=self.pool):
                 e.loss = self._body(e.batch)
         finally:
             setup.graph_inputs = None

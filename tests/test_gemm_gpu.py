@@ -133,7 +133,7 @@ def test_autotuned_plans(dev, autotune):
     n = len(K.gemm_autotune_cache())
     assert n >= 5
     for t, s in K.gemm_autotune_cache().values():
-        assert -1 <= t <= 5 and s >= 1
+        assert -1 <= t <= 4 and s >= 1
     K.linear(x, w, residual=r)           # cached: no new entries
     assert len(K.gemm_autotune_cache()) == n
 
@@ -174,45 +174,3 @@ def test_every_tile_explicit(dev, tile, monkeypatch):
         close(dxc, to_nhwc(refd))
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
-def test_splitk_fixup_matches_reduce_kernel(dev, tile, monkeypatch):
-    """Split-K partials summed in-kernel by each tile's last-arriving workgroup give the same bits as
-    the separate splitk_reduce_kernel (OTAMD_SPLITK_FIXUP=0): 8- and 4-wide (N % 8 != 0) epilogues,
-    bias + residual, fp32 accumulate, ragged tiles, 2..7 splits."""
-    torch.manual_seed(5)
-    plan = {"s": 2}
-
-    def explicit(a, s_, device):
-        sp = plan["s"]
-        ws_bytes = sp * a.M * a.N * 4
-        ws = K.workspace(ws_bytes, device)
-        K.check(K.lib().otamd_gemm_explicit(C.byref(a), tile, sp, K._p(ws), ws_bytes, K.stream_handle()),
-                "otamd_gemm_explicit")
-
-    monkeypatch.setattr(K, "_gemm", explicit)
-    x, w, b = rnd(1000, 2048, dev=dev), rnd(328, 2048, dev=dev, scale=0.05), rnd(328, dev=dev)
-    r = rnd(1000, 328, dev=dev)
-    w4 = rnd(300, 2048, dev=dev, scale=0.05)
-    dy, xt = rnd(4096, 328, dev=dev), rnd(4096, 264, dev=dev)
-    acc0 = torch.randn(328, 264, device=dev)
-
-    def run():
-        y = K.linear(x, w, bias=b, residual=r)
-        y4 = K.linear(x, w4)
-        g = acc0.clone()
-        K.linear_wgrad(dy, xt, out=g, accumulate=True)
-        torch.cuda.synchronize()
-        return y, y4, g
-
-    for s in (2, 3, 7):
-        plan["s"] = s
-        monkeypatch.setenv("OTAMD_SPLITK_FIXUP", "0")
-        ref = run()
-        monkeypatch.setenv("OTAMD_SPLITK_FIXUP", "1")
-        for rep in range(2):   # twice: the per-stream counters must be back at zero
-            out = run()
-            for o, e in zip(out, ref):
-                assert torch.equal(o, e), (tile, s, rep)
-    close(out[0], x.float() @ w.float().t() + b.float() + r.float())
-    close(out[1], x.float() @ w4.float().t())
-    close(out[2], acc0 + dy.float().t() @ xt.float(), tol=1e-2)
