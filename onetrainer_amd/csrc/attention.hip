@@ -26,6 +26,8 @@
 #include <cstdlib>
 #include <mutex>
 #include <unordered_set>
+#include <utility>
+#include <type_traits>
 
 struct AttnArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; bf16_t* o; float* lse;
@@ -126,6 +128,48 @@ __device__ __forceinline__ float xor32(float x) {
   return __uint_as_float((threadIdx.x & 32) ? s[0] : s[1]);
 }
 
+// 32 rows x 32 columns of fp32 accumulators (one 32x32 MFMA tile; lane (r, h) holds columns
+// 8g + 4h .. +3 of row r for g = 0..3) -> bf16 row segments of `row` starting at col0, scaled by
+// `mul`.  Column groups are paired with v_permlane32_swap so each lane stores 16 contiguous bytes
+// (cdna_hip_programming.md T21): 2 dwordx4 stores per lane instead of 4 dwordx2.  All 64 lanes
+// execute the swaps; `ok` (row in range) gates only the stores.  Needs 16-byte aligned rows.
+__device__ __forceinline__ void store_tile_bf16(bf16_t* row, int col0, const float16v& x, float mul, int Dv, bool ok) {
+  const int h = (threadIdx.x >> 5) & 1;
+#pragma unroll
+  for (int g = 0; g < 4; g += 2) {
+    const uint32_t a0 = (uint32_t)f2bf(x[4 * g] * mul) | ((uint32_t)f2bf(x[4 * g + 1] * mul) << 16);
+    const uint32_t a1 = (uint32_t)f2bf(x[4 * g + 2] * mul) | ((uint32_t)f2bf(x[4 * g + 3] * mul) << 16);
+    const uint32_t b0 = (uint32_t)f2bf(x[4 * g + 4] * mul) | ((uint32_t)f2bf(x[4 * g + 5] * mul) << 16);
+    const uint32_t b1 = (uint32_t)f2bf(x[4 * g + 6] * mul) | ((uint32_t)f2bf(x[4 * g + 7] * mul) << 16);
+    const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    const int c = col0 + 8 * g + 8 * h;
+    if (ok && c < Dv) *reinterpret_cast<uint4*>(row + c) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  }
+}
+
+// The tile loop unrolled by the ring depth NS: the ring slot t % NS is a compile-time constant in
+// every copy of the body, so every LDS address is a lane base + an immediate offset (no per-tile
+// address VALU).  step(t, std::integral_constant<int, t % NS>).
+template <typename F, int... I>
+__device__ __forceinline__ void stage_steps(int t, F& step, std::integer_sequence<int, I...>) {
+  (step(t + I, std::integral_constant<int, I>{}), ...);
+}
+template <typename F, int... I>
+__device__ __forceinline__ void stage_tail(int t, int n, F& step, std::integer_sequence<int, I...>) {
+  ((t + I < n ? step(t + I, std::integral_constant<int, I>{}) : void()), ...);
+}
+template <int NS, bool UNROLL = true, typename F>
+__device__ __forceinline__ void stage_loop(int ntiles, F&& step) {
+  if constexpr (UNROLL) {
+    int t = 0;
+    for (; t + NS <= ntiles; t += NS) stage_steps(t, step, std::make_integer_sequence<int, NS>{});
+    stage_tail(t, ntiles, step, std::make_integer_sequence<int, NS - 1>{});
+  } else {   // (D = 128: the unrolled copies would not fit the register budget)
+    for (int t = 0; t < ntiles; ++t) step(t, t % NS);
+  }
+}
+
 // DMA geometry of one [ROWS x D] bf16 image (row or transposed-read swizzle), split over 4 waves:
 // piece p (1 KiB) = wave + 4 i; lane l writes bytes [16 l, 16 l + 16) of the piece.
 template <int D, int ROWS, bool TR>
@@ -182,12 +226,13 @@ __device__ __forceinline__ void exp2_scaled(float16v& S, float c, float bias) {
 }
 
 // ------------------------------------------------------------------------------------------
-template <int D>
+// NS = LDS ring depth.  D = 128 runs NS = 2 (64 KiB): two blocks (8 waves) per CU instead of one
+// with the 96 KiB 3-deep ring -- the MFMA of one wave overlaps the softmax of the SIMD's other wave.
+template <int D, int NS>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = KT * D * 2;      // bytes of one [64 x D] image
   constexpr int STG = 2 * TB;         // K row image + V transposed-read image
-  constexpr int NS = 3;
   using KImg = DmaImg<D, KT, false>;
   using VImg = DmaImg<D, KT, true>;
   constexpr int LOADS = KImg::PW + VImg::PW;
@@ -221,16 +266,18 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t) O[t] = zero16();
   float m = -INFINITY, l = 0.f;
 
-  for (int t = 0; t < ntiles; ++t) {
+  auto step = [&](int t, auto si_tag) {
+    const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
+
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
     BARRIER();
     if (t + NS - 1 < ntiles) {
-      char* st = smem + ((t + NS - 1) % NS) * STG;
+      char* st = smem + ((SI + NS - 1) % NS) * STG;
       ki.issue(rk, st, a.ldk, (t + NS - 1) * KT, a.Nk, a.Dv, wave);
       vi.issue(rv, st + TB, a.ldv, (t + NS - 1) * KT, a.Nk, a.Dv, wave);
     }
-    const char* kimg = smem + (t % NS) * STG;
+    const char* kimg = smem + SI * STG;
     const char* vimg = kimg + TB;
 #pragma unroll
     for (int sub = 0; sub < KT / 32; ++sub) {
@@ -278,38 +325,28 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         O[dt] = mfma32(tr_frag<D>(vimg, sub * 32, 1, dt * 32), p1, O[dt]);
       }
     }
-  }
+  };
+  stage_loop<NS, (D <= 64)>(ntiles, step);
   const int q = q0 + r;
-  if (q < a.Nq) {
-    const float inv = 1.f / l;
-    bf16_t* Op = a.o + b * a.bso + (long long)q * a.ldo + hh * a.Dv;
+  const float inv = 1.f / l;
+  bf16_t* Op = a.o + b * a.bso + (long long)min(q, a.Nq - 1) * a.ldo + hh * a.Dv;
 #pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * h;
-        if (d < a.Dv) {
-          uint2 w;
-          w.x = (uint32_t)f2bf(O[dt][4 * g] * inv) | ((uint32_t)f2bf(O[dt][4 * g + 1] * inv) << 16);
-          w.y = (uint32_t)f2bf(O[dt][4 * g + 2] * inv) | ((uint32_t)f2bf(O[dt][4 * g + 3] * inv) << 16);
-          *reinterpret_cast<uint2*>(Op + d) = w;
-        }
-      }
-    if (h == 0 && a.lse) a.lse[((long long)b * a.H + hh) * a.Nq + q] = m + __log2f(l);
-  }
+  for (int dt = 0; dt < D / 32; ++dt) store_tile_bf16(Op, dt * 32, O[dt], inv, a.Dv, q < a.Nq);
+  if (q < a.Nq && h == 0 && a.lse) a.lse[((long long)b * a.H + hh) * a.Nq + q] = m + __log2f(l);
 }
 
 // dQ: per wave 32 queries, iterate over key tiles (K row + K transposed + V row images per stage)
-// NS = LDS ring depth.  D = 64 with NS = 2 (48 KiB) lets three blocks share a CU (150 VGPRs fit three
+// NS = LDS ring depth, KTD = keys per tile.  D = 128 runs 32-key tiles 3 deep (72 KiB): two blocks
+// per CU (the 64-key 3-deep ring, 144 KiB, left one block -- one wave per SIMD).  D = 64 with NS = 2 (48 KiB) lets three blocks share a CU (150 VGPRs fit three
 // waves per SIMD), so the SDXL level-2 grid (8 x 20 heads x 4 = 640 blocks) runs in one round of
 // 768 slots instead of 1.25 rounds of 512 with NS = 3 (72 KiB).
-template <int D, int NS>
+template <int D, int NS, int KTD = KT>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TB = KT * D * 2;
+  constexpr int TB = KTD * D * 2;
   constexpr int STG = 3 * TB;
-  using RImg = DmaImg<D, KT, false>;
-  using TImg = DmaImg<D, KT, true>;
+  using RImg = DmaImg<D, KTD, false>;
+  using TImg = DmaImg<D, KTD, true>;
   constexpr int LOADS = 2 * RImg::PW + TImg::PW;
   const int b = blockIdx.z, hh = blockIdx.y;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -321,11 +358,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   TImg ti;
   ri.prepare(wave, lane);
   ti.prepare(wave, lane);
-  const int ntiles = (a.Nk + KT - 1) / KT;
+  const int ntiles = (a.Nk + KTD - 1) / KTD;
   auto issue = [&](int t, char* st) {
-    ri.issue(rk, st, a.ldk, t * KT, a.Nk, a.Dv, wave);
-    ti.issue(rk, st + TB, a.ldk, t * KT, a.Nk, a.Dv, wave);
-    ri.issue(rv, st + 2 * TB, a.ldv, t * KT, a.Nk, a.Dv, wave);
+    ri.issue(rk, st, a.ldk, t * KTD, a.Nk, a.Dv, wave);
+    ti.issue(rk, st + TB, a.ldk, t * KTD, a.Nk, a.Dv, wave);
+    ri.issue(rv, st + 2 * TB, a.ldv, t * KTD, a.Nk, a.Dv, wave);
   };
 
   bf16x8 qf[D / 16], gf[D / 16];
@@ -366,23 +403,25 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dQ[t] = zero16();
 
-  for (int t = 0; t < ntiles; ++t) {
+  auto step = [&](int t, auto si_tag) {
+    const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
+
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
     BARRIER();
-    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((t + NS - 1) % NS) * STG);
-    const char* krow = smem + (t % NS) * STG;
+    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
+    const char* krow = smem + SI * STG;
     const char* ktr = krow + TB;
     const char* vrow = krow + 2 * TB;
 #pragma unroll
-    for (int sub = 0; sub < KT / 32; ++sub) {
+    for (int sub = 0; sub < KTD / 32; ++sub) {
       float16v S = zero16(), dP = zero16();
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
         S = mfma32(lds_row_frag(krow, D * 2, sub * 32 + r, 2 * s + h), qf[s], S);
         dP = mfma32(lds_row_frag(vrow, D * 2, sub * 32 + r, 2 * s + h), gf[s], dP);
       }
-      const int kbase = t * KT + sub * 32;
+      const int kbase = t * KTD + sub * 32;
       if (kbase + 32 > a.Nk) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
@@ -403,22 +442,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
         dQ[dt] = mfma32(tr_frag<D>(ktr, sub * 32, 1, dt * 32), s1, dQ[dt]);
       }
     }
-  }
-  if (q < a.Nq) {
-    bf16_t* Dp = a.dq + b * a.bsdq + (long long)q * a.lddq + hh * a.Dv;
+  };
+  stage_loop<NS, (D <= 64)>(ntiles, step);
+  bf16_t* Dp = a.dq + b * a.bsdq + (long long)min(q, a.Nq - 1) * a.lddq + hh * a.Dv;
 #pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * h;
-        if (d < a.Dv) {
-          uint2 w;
-          w.x = (uint32_t)f2bf(dQ[dt][4 * g] * a.scale) | ((uint32_t)f2bf(dQ[dt][4 * g + 1] * a.scale) << 16);
-          w.y = (uint32_t)f2bf(dQ[dt][4 * g + 2] * a.scale) | ((uint32_t)f2bf(dQ[dt][4 * g + 3] * a.scale) << 16);
-          *reinterpret_cast<uint2*>(Dp + d) = w;
-        }
-      }
-  }
+  for (int dt = 0; dt < D / 32; ++dt) store_tile_bf16(Dp, dt * 32, dQ[dt], a.scale, a.Dv, q < a.Nq);
 }
 
 // dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of 32 in this split's range.
@@ -480,12 +508,14 @@ __global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(Attn
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) { dK[t] = zero16(); dV[t] = zero16(); }
 
-  for (int t = 0; t < ntiles; ++t) {
+  auto step = [&](int t, auto si_tag) {
+    const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
+
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
     BARRIER();
-    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((t + NS - 1) % NS) * STG);
-    const char* st = smem + (t % NS) * STG;
+    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
+    const char* st = smem + SI * STG;
     const char* qrow = st;
     const char* qtr = st + TB;
     const char* grow = st + 2 * TB;
@@ -525,7 +555,8 @@ __global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(Attn
       dK[dt] = mfma32(tr_frag<D>(qtr, 0, 0, dt * 32), s0, dK[dt]);
       dK[dt] = mfma32(tr_frag<D>(qtr, 0, 1, dt * 32), s1, dK[dt]);
     }
-  }
+  };
+  stage_loop<NS, (D <= 64)>(ntiles, step);
   const int key = k0 + r;
   if (key < a.Nk) {
 #pragma unroll
@@ -541,18 +572,17 @@ __global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(Attn
                           dK[dt][4 * g + 3] * a.scale);
           *reinterpret_cast<float4*>(a.dv32 + base) =
               make_float4(dV[dt][4 * g], dV[dt][4 * g + 1], dV[dt][4 * g + 2], dV[dt][4 * g + 3]);
-        } else {
-          bf16_t* kp = a.dk + b * a.bsdk + (long long)key * a.lddk + hh * a.Dv + d;
-          bf16_t* vp = a.dv + b * a.bsdv + (long long)key * a.lddv + hh * a.Dv + d;
-          uint2 w;
-          w.x = (uint32_t)f2bf(dK[dt][4 * g] * a.scale) | ((uint32_t)f2bf(dK[dt][4 * g + 1] * a.scale) << 16);
-          w.y = (uint32_t)f2bf(dK[dt][4 * g + 2] * a.scale) | ((uint32_t)f2bf(dK[dt][4 * g + 3] * a.scale) << 16);
-          *reinterpret_cast<uint2*>(kp) = w;
-          w.x = (uint32_t)f2bf(dV[dt][4 * g]) | ((uint32_t)f2bf(dV[dt][4 * g + 1]) << 16);
-          w.y = (uint32_t)f2bf(dV[dt][4 * g + 2]) | ((uint32_t)f2bf(dV[dt][4 * g + 3]) << 16);
-          *reinterpret_cast<uint2*>(vp) = w;
         }
       }
+  }
+  if (a.qsplit == 1) {
+    bf16_t* kp = a.dk + b * a.bsdk + (long long)min(key, a.Nk - 1) * a.lddk + hh * a.Dv;
+    bf16_t* vp = a.dv + b * a.bsdv + (long long)min(key, a.Nk - 1) * a.lddv + hh * a.Dv;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+      store_tile_bf16(kp, dt * 32, dK[dt], a.scale, a.Dv, key < a.Nk);
+      store_tile_bf16(vp, dt * 32, dV[dt], 1.f, a.Dv, key < a.Nk);
+    }
   }
 }
 
@@ -612,10 +642,10 @@ static void launch(K kern, dim3 grid, int lds, hipStream_t s, const AttnArgs& a)
 OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
   if (!in || !attn_ok(*in) || !in->o || !in->lse) return OTAMD_EINVAL;
   AttnArgs a = *in;
-  if (a.ldo % 4 || a.bso % 4) return OTAMD_EINVAL;
+  if (a.ldo % 8 || a.bso % 8 || ((uintptr_t)a.o & 15)) return OTAMD_EINVAL;   // 16-byte row stores
   dim3 grid((a.Nq + 127) / 128, a.H, a.B);
-  if (a.Dv <= 64) launch(attn_fwd_kernel<64>, grid, 3 * 2 * KT * 64 * 2, stream, a);
-  else launch(attn_fwd_kernel<128>, grid, 3 * 2 * KT * 128 * 2, stream, a);
+  if (a.Dv <= 64) launch(attn_fwd_kernel<64, 3>, grid, 3 * 2 * KT * 64 * 2, stream, a);
+  else launch(attn_fwd_kernel<128, 2>, grid, 2 * 2 * KT * 128 * 2, stream, a);   // 369 vs 512 us (NS = 3), Flux 2381 tokens
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
@@ -640,7 +670,9 @@ OTAMD_API long long otamd_attn_bwd_ws_bytes(const AttnArgs* in) {
 OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream) {
   if (!in || !attn_ok(*in) || !in->o || !in->lse || !in->dout || !in->dq || !in->dk || !in->dv || !ws) return OTAMD_EINVAL;
   AttnArgs a = *in;
-  if (a.lddo % 8 || a.bsdo % 8 || a.lddq % 4 || a.lddk % 4 || a.lddv % 4 || ((uintptr_t)ws & 15)) return OTAMD_EINVAL;
+  if (a.lddo % 8 || a.bsdo % 8 || a.lddq % 8 || a.lddk % 8 || a.lddv % 8 || a.bsdq % 8 || a.bsdk % 8 || a.bsdv % 8 ||
+      (((uintptr_t)ws | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
+    return OTAMD_EINVAL;   // 16-byte row stores
   if (((uintptr_t)a.dout & 15) || !fits31(a.Nq, a.lddo)) return OTAMD_EINVAL;
   const long long nrow = (long long)a.B * a.H * a.Nq;
   const long long nkv = (long long)a.B * a.Nk * a.H * a.Dv;
@@ -661,7 +693,7 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
     else launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
     launch(attn_bwd_dkv_kernel<64>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);
   } else {
-    launch(attn_bwd_dq_kernel<128, 3>, gq, 3 * 3 * KT * 128 * 2, stream, a);
+    launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // bwd 1349 vs 1467 us (64-key tiles)
     launch(attn_bwd_dkv_kernel<128>, gk, 3 * (4 * QT * 128 * 2 + QT * 8), stream, a);
   }
   OTAMD_CHECK_LAUNCH();

@@ -1,4 +1,4 @@
-"""GEMM census of one SDXL train step (1024^2, b=4): every GEMM/conv launch timed on the GPU with
+"""GEMM census of one SDXL (1024^2, b=4) or FLUX.1 LoRA (768^2, b=4) train step: every GEMM/conv launch timed on the GPU with
 events around it (includes the split-K reduce), grouped by (A mode, B mode, M, N, K, tile, splits).
 Prints one JSON line per group, sorted by total time, plus the total.
 
@@ -29,16 +29,24 @@ def main():
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--lora", type=int, default=0, help="LoRA rank (0: full fine-tune)")
+    ap.add_argument("--flux", action="store_true", help="FLUX.1 LoRA r16 (C5) at --res (default 768)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = TrainConfig.default_values()
     cfg.batch_size = args.batch
     if args.lora:
         cfg.training_method, cfg.lora_rank = "LORA", args.lora
-    model = create.create_model(cfg, dev, seed=0)
-    tr = GenericTrainer(cfg, model=model)
+    if args.flux:
+        cfg.model_type, cfg.training_method, cfg.timestep_distribution = "FLUX_DEV_1", "LORA", "LOGIT_NORMAL"
+        if args.res == 1024:
+            args.res = 768
+    tr = GenericTrainer(cfg) if args.flux else GenericTrainer(cfg, model=create.create_model(cfg, dev, seed=0))
     tr.start()
-    batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=0)
+    if args.flux:
+        from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_flux_batch
+        batch = synthetic_flux_batch(args.batch, args.res, args.res, dev, seed=0)
+    else:
+        batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=0)
     tr.train_step(batch)
     torch.cuda.synchronize()
 
