@@ -228,8 +228,9 @@ __device__ __forceinline__ void exp2_scaled(float16v& S, float c, float bias) {
 // ------------------------------------------------------------------------------------------
 // NS = LDS ring depth.  D = 128 runs NS = 2 (64 KiB): two blocks (8 waves) per CU instead of one
 // with the 96 KiB 3-deep ring -- the MFMA of one wave overlaps the softmax of the SIMD's other wave.
+// D = 64 runs NS = 2 (32 KiB) at <= 128 VGPRs: four blocks, four waves per SIMD.
 template <int D, int NS>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = KT * D * 2;      // bytes of one [64 x D] image
   constexpr int STG = 2 * TB;         // K row image + V transposed-read image
@@ -453,6 +454,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 // Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 {lse, delta} pairs.
 // D = 128: the dK/dV accumulators alone take 128 VGPRs and the 3-deep ring (99 KiB) already limits a
 // CU to one block, so the full 512-entry register file is used instead of spilling at 256.
+// (A software-pipelined D = 128 variant -- S / dP of tile t+1 on the MFMA pipe during tile t's
+// softmax, 4-deep ring -- measured slower: 1487-1510 vs 1349 us for the Flux bwd; not kept.)
 template <int D>
 __global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -508,25 +511,19 @@ __global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(Attn
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) { dK[t] = zero16(); dV[t] = zero16(); }
 
-  auto step = [&](int t, auto si_tag) {
-    const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
-
-    if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
-    else wait_vmcnt<0>();
-    BARRIER();
-    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
-    const char* st = smem + SI * STG;
-    const char* qrow = st;
-    const char* qtr = st + TB;
-    const char* grow = st + 2 * TB;
-    const char* gtr = st + 3 * TB;
-    const float4* pv = reinterpret_cast<const float4*>(st + 4 * TB);   // pv[j] = pairs 2j, 2j+1
-    float16v S = zero16(), dP = zero16();
+  // S = Q K^T and dP = dO V^T of one query tile (key on the lane)
+  auto sdp = [&](float16v& S_, float16v& dP_, const char* st) {
+    S_ = zero16();
+    dP_ = zero16();
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
-      S = mfma32(lds_row_frag(qrow, D * 2, r, 2 * s + h), kf[s], S);
-      dP = mfma32(lds_row_frag(grow, D * 2, r, 2 * s + h), vf[s], dP);
+      S_ = mfma32(lds_row_frag(st, D * 2, r, 2 * s + h), kf[s], S_);
+      dP_ = mfma32(lds_row_frag(st + 2 * TB, D * 2, r, 2 * s + h), vf[s], dP_);
     }
+  };
+  // P = exp2(S c - lse), dS = P (dP - delta), packed as the dV / dK B operands
+  auto softmax_pack = [&](float16v& S, float16v& dP, const char* st, bf16x8 (&pk)[4]) {
+    const float4* pv = reinterpret_cast<const float4*>(st + 4 * TB);   // pv[j] = pairs 2j, 2j+1
 #pragma unroll
     for (int g = 0; g < 4; ++g) {      // registers 4g..4g+3 <-> queries 8g + 4h + (0..3)
       const int q4 = 8 * g + 4 * h;
@@ -546,15 +543,37 @@ __global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(Attn
         dP[4 * g + 2 * e + 1] = d.y;
       }
     }
-    const bf16x8 p0 = pack_acc(S, 0), p1 = pack_acc(S, 1);
-    const bf16x8 s0 = pack_acc(dP, 0), s1 = pack_acc(dP, 1);
+    pk[0] = pack_acc(S, 0);
+    pk[1] = pack_acc(S, 1);
+    pk[2] = pack_acc(dP, 0);
+    pk[3] = pack_acc(dP, 1);
+  };
+  // dV^T += dO^T P, dK^T += Q^T dS
+  auto dvdk = [&](const char* st, const bf16x8 (&pk)[4]) {
+    const char* qtr = st + TB;
+    const char* gtr = st + 3 * TB;
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt) {
-      dV[dt] = mfma32(tr_frag<D>(gtr, 0, 0, dt * 32), p0, dV[dt]);
-      dV[dt] = mfma32(tr_frag<D>(gtr, 0, 1, dt * 32), p1, dV[dt]);
-      dK[dt] = mfma32(tr_frag<D>(qtr, 0, 0, dt * 32), s0, dK[dt]);
-      dK[dt] = mfma32(tr_frag<D>(qtr, 0, 1, dt * 32), s1, dK[dt]);
+      dV[dt] = mfma32(tr_frag<D>(gtr, 0, 0, dt * 32), pk[0], dV[dt]);
+      dV[dt] = mfma32(tr_frag<D>(gtr, 0, 1, dt * 32), pk[1], dV[dt]);
+      dK[dt] = mfma32(tr_frag<D>(qtr, 0, 0, dt * 32), pk[2], dK[dt]);
+      dK[dt] = mfma32(tr_frag<D>(qtr, 0, 1, dt * 32), pk[3], dK[dt]);
     }
+  };
+
+
+  auto step = [&](int t, auto si_tag) {
+    const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
+    if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
+    else wait_vmcnt<0>();
+    BARRIER();
+    if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
+    const char* st = smem + SI * STG;
+    float16v S, dP;
+    bf16x8 pk[4];
+    sdp(S, dP, st);
+    softmax_pack(S, dP, st, pk);
+    dvdk(st, pk);
   };
   stage_loop<NS, (D <= 64)>(ntiles, step);
   const int key = k0 + r;
@@ -644,7 +663,7 @@ OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
   AttnArgs a = *in;
   if (a.ldo % 8 || a.bso % 8 || ((uintptr_t)a.o & 15)) return OTAMD_EINVAL;   // 16-byte row stores
   dim3 grid((a.Nq + 127) / 128, a.H, a.B);
-  if (a.Dv <= 64) launch(attn_fwd_kernel<64, 3>, grid, 3 * 2 * KT * 64 * 2, stream, a);
+  if (a.Dv <= 64) launch(attn_fwd_kernel<64, 2>, grid, 2 * 2 * KT * 64 * 2, stream, a);   // 4 waves/SIMD: 279 vs 288 us
   else launch(attn_fwd_kernel<128, 2>, grid, 2 * 2 * KT * 128 * 2, stream, a);   // 369 vs 512 us (NS = 3), Flux 2381 tokens
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
@@ -687,10 +706,8 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   const int kblocks = (a.Nk + 127) / 128;
   dim3 gq((a.Nq + 127) / 128, a.H, a.B);
   dim3 gk(kblocks, a.H, a.B * qsplit);
-  static const bool dq3 = getenv("OTAMD_ATTN_DQ_NS3") && !strcmp(getenv("OTAMD_ATTN_DQ_NS3"), "1");   // A/B switch
   if (a.Dv <= 64) {
-    if (dq3) launch(attn_bwd_dq_kernel<64, 3>, gq, 3 * 3 * KT * 64 * 2, stream, a);
-    else launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
+    launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
     launch(attn_bwd_dkv_kernel<64>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);
   } else {
     launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // bwd 1349 vs 1467 us (64-key tiles)
