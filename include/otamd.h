@@ -99,7 +99,8 @@ long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out);
 int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                         hipStream_t stream);
 
-/* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves */
+/* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves,
+   4 128x128, 5 128x64, 6 64x128 */
 int otamd_gemm_plan_tile(const GemmArgs* in, int splits);
 
 /* replaces: ABI check */

@@ -168,6 +168,8 @@ __device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, in
 __device__ __forceinline__ int kimg_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 // MN-mode LDS image: [64 k rows][RB bytes], 32-byte block b of row k stored at b ^ s(k)
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+// the same for an image of RB-byte rows: a 64-wide tile (128-byte rows) has only 4 blocks per row
+template <int RB> __device__ __forceinline__ int mn_swz_rb(int k) { return RB >= 256 ? mn_swz(k) : (k & 3); }
 
 // alpha * sum_s slab[s] (+bias, +rowvec, +residual) (+C if accumulate) for V consecutive columns
 // n.. of row m: the split-K combine of splitk_reduce_kernel (splits summed in index order).

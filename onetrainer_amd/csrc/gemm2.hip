@@ -30,13 +30,8 @@ typedef __attribute__((address_space(3))) short4v lds_s4_t;
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else static_assert(N == 0, "unsupported vmcnt");
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // One 16-byte-per-lane LDS-DMA (1 KiB per wave). Issued as inline asm on purpose: the compiler's
@@ -86,7 +81,7 @@ struct Stage {
         const int byte = j * 1024 + lane * 16;
         const int r = byte / RB;
         const int pc = (byte % RB) >> 4;
-        const int lb = (pc >> 1) ^ mn_swz(r);
+        const int lb = (pc >> 1) ^ mn_swz_rb<RB>(r);
         const int col = mn0 + (lb * 2 + (pc & 1)) * 8;
         a[i] = r;
         ok[i] = col < MNsz;
@@ -179,7 +174,7 @@ __device__ __forceinline__ bf16x8 frag_k2(const char* img, int mnb, int kb) {
 }
 template <int RB>
 __device__ __forceinline__ int mn_off(int k, int col) {
-  return k * RB + ((((col >> 4)) ^ mn_swz(k)) << 5) + ((col & 15) << 1);
+  return k * RB + ((((col >> 4)) ^ mn_swz_rb<RB>(k)) << 5) + ((col & 15) << 1);
 }
 template <int RB>
 __device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
@@ -426,7 +421,9 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   else if (tile == 1) { fn = pick2<256, 128, 8>(a.amode, a.bmode, seg2); BNv = 128; }
   else if (tile == 2) { fn = pick2<128, 256, 8>(a.amode, a.bmode, seg2); BMv = 128; }
   else if (tile == 4) { fn = pick2<128, 128, 8>(a.amode, a.bmode, seg2); BMv = 128; BNv = 128; }
-  else if (!seg2) { fn = pick2<256, 256, 4>(a.amode, a.bmode, false); NWv = 4; }
+  else if (tile == 5) { fn = pick2<128, 64, 8>(a.amode, a.bmode, seg2); BMv = 128; BNv = 64; }
+  else if (tile == 6) { fn = pick2<64, 128, 8>(a.amode, a.bmode, seg2); BMv = 64; BNv = 128; }
+  else if (tile == 3 && !seg2) { fn = pick2<256, 256, 4>(a.amode, a.bmode, false); NWv = 4; }
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
   const int lds = 2 * (BMv + BNv) * 128;

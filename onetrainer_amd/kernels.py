@@ -63,7 +63,7 @@ _gemm_forced_splits = 0   # tools/gemm_splits.py probe: forces the split count o
 # otamd_gemm_explicit.  Candidate plans all compute the same product; they differ only in the fp32
 # summation order of split-K.
 _TUNE = {"on": False, "cache": {}, "reps": 3}
-_TILES = (0, 1, 2, 3, 4, -1)
+_TILES = (0, 1, 2, 3, 4, 5, 6, -1)
 _SPLITS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 16)
 
 
