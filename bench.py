@@ -172,8 +172,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true", help="skip the VAE-encode (latent caching) side measurement")
     ap.add_argument("--autotune", action="store_true",
-                    help="time (tile, split-K) candidates per GEMM signature in warm-up instead of the analytic plan "
-                         "(measured: no gain on the SDXL step -- isolated warm-cache timings do not transfer)")
+                    help="time (tile, split-K) candidates per GEMM signature in warm-up instead of the measured plan "
+                         "table / analytic plan")
+    ap.add_argument("--dump-plans", default=None,
+                    help="with --autotune: merge the tuned plans into this plan-table JSON (kernels.dump_plan_table)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
@@ -350,10 +352,13 @@ def main():
         "cpu_baseline": None,
         "vae_encode": vae,
         "gemm_plans": "autotuned in warm-up (%d signatures)" % len(K.gemm_autotune_cache()) if args.autotune
-        else "analytic",
+        else K.plan_source(),
         "step_graph": (f"forward+backward replayed as HIP graphs ({len(tr.graphs.entries)} captured shapes); "
                        f"noise/timesteps and the optimizer update eager") if tr.graphs is not None else "eager",
     }
+    if args.autotune and args.dump_plans and rank == 0:
+        n = K.dump_plan_table(args.dump_plans)
+        print(f"plan table: {n} signatures -> {args.dump_plans}", file=sys.stderr)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not flux and not sdxl_lora:
         del tr
         torch.cuda.empty_cache()

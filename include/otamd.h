@@ -54,7 +54,6 @@ typedef struct GemmArgs {
      (z / bdiv) * s0 + (z % bdiv) * s1 elements ((image, head) pairs of [B, N, H*D] activations) */
   int batch, bdiv;
   long long sa0, sa1, sb0, sb1, sc0, sc1;
-  unsigned* tile_ctr;   /* set by the library (split-K fix-up counters); callers leave it NULL */
 } GemmArgs;
 
 typedef struct AttnArgs {
@@ -94,13 +93,15 @@ int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long long ws_byt
 long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out);
 
 /* replaces: (plan override) the same GEMM with an explicit plan -- the autotuner's candidates and its
-   cached per-shape choice (kernels.py set_gemm_autotune).  tile: -1 v1 128x128, 0 256x256, 1 256x128,
-   2 128x256, 3 256x256/4 waves; splits >= 1; workspace >= splits*M*N*4 bytes when splits > 1 */
+   cached per-shape choice (kernels.py set_gemm_autotune) and the measured plan table
+   (onetrainer_amd/gemm_plans_mi355x.json).  tile: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256,
+   3 256x256/4 waves, 4 128x128/8 waves, 5 128x64, 6 64x128, 7 128x160, 8 256x160; splits >= 1;
+   workspace >= splits*M*N*4 bytes when splits > 1 */
 int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                         hipStream_t stream);
 
 /* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves,
-   4 128x128, 5 128x64, 6 64x128 */
+   4 128x128, 5 128x64, 6 64x128, 7 128x160, 8 256x160 */
 int otamd_gemm_plan_tile(const GemmArgs* in, int splits);
 
 /* replaces: ABI check */

@@ -169,7 +169,11 @@ __device__ __forceinline__ int kimg_off(int row, int chunk) { return row * 128 +
 // MN-mode LDS image: [64 k rows][RB bytes], 32-byte block b of row k stored at b ^ s(k)
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 // the same for an image of RB-byte rows: a 64-wide tile (128-byte rows) has only 4 blocks per row
-template <int RB> __device__ __forceinline__ int mn_swz_rb(int k) { return RB >= 256 ? mn_swz(k) : (k & 3); }
+// and 160-wide tiles (320-byte rows, 10 blocks): the 80-dword row pitch already spreads rows k..k+3 over
+// four 8-bank groups; rows k+8.. alias them, so block bit 0 flips with k bit 3 (stays inside the row)
+template <int RB> __device__ __forceinline__ int mn_swz_rb(int k) {
+  return RB == 320 ? ((k >> 3) & 1) : (RB >= 256 ? mn_swz(k) : (k & 3));
+}
 
 // alpha * sum_s slab[s] (+bias, +rowvec, +residual) (+C if accumulate) for V consecutive columns
 // n.. of row m: the split-K combine of splitk_reduce_kernel (splits summed in index order).

@@ -330,6 +330,8 @@ static int forced_tile() {
       else if (!strcmp(e, "128x128w8")) forced = 4;
       else if (!strcmp(e, "128x64")) forced = 5;
       else if (!strcmp(e, "64x128")) forced = 6;
+      else if (!strcmp(e, "128x160")) forced = 7;
+      else if (!strcmp(e, "256x160")) forced = 8;
     }
   }
   return forced;
@@ -344,10 +346,13 @@ struct TileCand { int tile, bm, bn, per_cu; double rate, fixed; };
 // Tiles 5 (128x64) and 6 (64x128): the skinny LoRA GEMMs (t = x A^T and u = dy B with N = rank,
 // the adapter wgrads with M or N = rank), where a 128- or 256-wide tile spends 2-8x the MFMA work
 // on zero padding; three workgroups per CU (48 KiB of LDS each).
-static const TileCand kTiles[7] = {{-1, 128, 128, 2, 0.55, 2.5e-6}, {0, 256, 256, 1, 1.0, 2.5e-6},
+// Tiles 7 (128x160) and 8 (256x160): N = 320 / 640 / 1280 without padding and 256 tiles for the
+// 4096 x 1280 and 16384 x 640 shapes; rates fitted to the tools/gemm_tiles.py sweep of the SDXL step.
+static const TileCand kTiles[9] = {{-1, 128, 128, 2, 0.55, 2.5e-6}, {0, 256, 256, 1, 1.0, 2.5e-6},
                                    {1, 256, 128, 1, 0.85, 2.5e-6}, {2, 128, 256, 1, 0.85, 2.5e-6},
                                    {4, 128, 128, 2, 0.85, 0.6e-6}, {5, 128, 64, 3, 0.55, 0.6e-6},
-                                   {6, 64, 128, 3, 0.55, 0.6e-6}};
+                                   {6, 64, 128, 3, 0.55, 0.6e-6}, {7, 128, 160, 2, 0.9, 4e-6},
+                                   {8, 256, 160, 1, 0.9, 2.5e-6}};
 
 static bool no_tile4() {   // OTAMD_GEMM_NO_T4=1: plan without the 128x128 tile (A/B measurements)
   static const bool v = getenv("OTAMD_GEMM_NO_T4") && !strcmp(getenv("OTAMD_GEMM_NO_T4"), "1");
@@ -403,7 +408,7 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
 
 // the tile otamd_gemm would launch for these arguments and splits (0 = automatic): -1 = v1 128x128,
 // 0 = 256x256, 1 = 256x128, 2 = 128x256 (8 waves), 3 = 256x256 (4 waves), 4 = 128x128 (8 waves),
-// 5 = 128x64, 6 = 64x128
+// 5 = 128x64, 6 = 64x128, 7 = 128x160, 8 = 256x160
 OTAMD_API int otamd_gemm_plan_tile(const GemmArgs* in, int splits) {
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -9;
   const bool v2_only = in->bmode == OPM_CONV_WT || in->A2 != nullptr;
@@ -507,11 +512,11 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
 
 // explicit plan (the autotuner's candidates and its cached choice): tile -1 = v1 128x128, 0 = 256x256,
 // 1 = 256x128, 2 = 128x256, 3 = 256x256 (4 waves), 4 = 128x128 (8 waves, 2 workgroups per CU),
-// 5 = 128x64, 6 = 64x128 (3 workgroups per CU);
+// 5 = 128x64, 6 = 64x128 (3 workgroups per CU), 7 = 128x160, 8 = 256x160;
 // splits >= 1 (rounded to whole 64-deep K steps)
 OTAMD_API int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                                   hipStream_t stream) {
-  if (tile < -1 || tile > 6 || splits < 1) return OTAMD_EINVAL;
+  if (tile < -1 || tile > 8 || splits < 1) return OTAMD_EINVAL;
   return gemm_impl(in, splits, tile, workspace, ws_bytes, stream);
 }
 

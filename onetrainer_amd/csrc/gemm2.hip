@@ -52,7 +52,9 @@ template <int MODE> struct IsKMode {
 template <int MODE, int BMN, int NW>
 struct Stage {
   static constexpr bool KM = IsKMode<MODE>::v;
-  static constexpr int NI = BMN / (8 * NW);
+  static constexpr int NP = BMN / 8;                  // 1 KiB pieces per stage image
+  static constexpr int NI = (NP + NW - 1) / NW;       // pieces per wave (the last may be absent)
+  static constexpr bool EVEN = NP % NW == 0;          // 160-wide images: 20 pieces over 8 waves
   static constexpr int RB = BMN * 2;      // MN-mode row bytes
   int a[NI], b[NI], c[NI];                // K: (row elem offset | conv n,y0,x0) ; MN: (k row, col, -)
   int t0, t1, t2;                         // K: logical chunk ; MN-conv: per-piece decode lives in a/b/c
@@ -133,7 +135,7 @@ struct Stage {
           }
           if (v) off = (unsigned)(((a[i] * g.SH + sy) * g.SW + sx) * (int)g.ld + ch) * 2u;
         }
-        dma16(rs, img + (wave + NW * i) * 1024, off);
+        if (EVEN || wave + NW * i < NP) dma16(rs, img + (wave + NW * i) * 1024, off);
       }
     } else {
 #pragma unroll
@@ -160,7 +162,7 @@ struct Stage {
           else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
           if (v) off = (unsigned)(((n * g.SH + sy) * g.SW + sx) * (int)g.ld + c[i]) * 2u;
         }
-        dma16(rs, img + (wave + NW * i) * 1024, off);
+        if (EVEN || wave + NW * i < NP) dma16(rs, img + (wave + NW * i) * 1024, off);
       }
     }
   }
@@ -192,10 +194,11 @@ __device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
 // unified VGPR/AGPR file), 256x256 as 2x2 wave tiles of 128x128 -- a third less LDS read traffic
 // per MFMA (one 16x16x32 fragment read per 4 MFMAs instead of per 2.7).
 template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2>
-__global__ void __launch_bounds__(NW * 64, (BM == 128 && BN == 128) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
+__global__ void __launch_bounds__(NW * 64, (BM == 128 && (BN == 128 || BN == 160)) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
                                                                  unsigned a2_bytes, unsigned b2_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int WN = NW == 4 ? 2 : ((BM == 256 && BN == 128) ? 2 : 4);
+  // BN = 160 (N = 320 / 640 / 1280 in 2 / 4 / 8 tiles, no padding): waves 4 x 2, wave tile (BM/4) x 80
+  constexpr int WN = NW == 4 ? 2 : ((BM == 256 && BN == 128) || BN == 160 ? 2 : 4);
   constexpr int WM = NW / WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MI = TM / 16, NJ = TN / 16;
@@ -203,6 +206,8 @@ __global__ void __launch_bounds__(NW * 64, (BM == 128 && BN == 128) ? 4 : NW / 4
   constexpr int STAGE = ABYTES + BBYTES;
   constexpr int LOADS = Stage<AM, BM, NW>::NI + Stage<BMODE, BN, NW>::NI;
   constexpr bool AK = IsKMode<AM>::v, BKm = IsKMode<BMODE>::v;
+  // per-wave DMA counts differ when an image does not split evenly: the prologue then drains fully
+  constexpr bool EVEN_LOADS = Stage<AM, BM, NW>::EVEN && Stage<BMODE, BN, NW>::EVEN && (!SEG2 || (Stage<OPM_K, BM, NW>::EVEN && Stage<BKm ? OPM_K : OPM_MN, BN, NW>::EVEN));
   if constexpr (!SEG2 && AM <= OPM_MN && BMODE <= OPM_MN) gemm_batch_offset(args);
 
   const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
@@ -291,7 +296,8 @@ __global__ void __launch_bounds__(NW * 64, (BM == 128 && BN == 128) ? 4 : NW / 4
     issue_tile(smem, kbeg);
     if (nk > 1) {
       issue_tile(smem + STAGE, kbeg + 64);
-      wait_vmcnt<LOADS>();
+      if constexpr (EVEN_LOADS) wait_vmcnt<LOADS>();
+      else wait_vmcnt<0>();
     } else {
       wait_vmcnt<0>();
     }
@@ -423,6 +429,8 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   else if (tile == 4) { fn = pick2<128, 128, 8>(a.amode, a.bmode, seg2); BMv = 128; BNv = 128; }
   else if (tile == 5) { fn = pick2<128, 64, 8>(a.amode, a.bmode, seg2); BMv = 128; BNv = 64; }
   else if (tile == 6) { fn = pick2<64, 128, 8>(a.amode, a.bmode, seg2); BMv = 64; BNv = 128; }
+  else if (tile == 7) { fn = pick2<128, 160, 8>(a.amode, a.bmode, seg2); BMv = 128; BNv = 160; }
+  else if (tile == 8) { fn = pick2<256, 160, 8>(a.amode, a.bmode, seg2); BNv = 160; }
   else if (tile == 3 && !seg2) { fn = pick2<256, 256, 4>(a.amode, a.bmode, false); NWv = 4; }
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);

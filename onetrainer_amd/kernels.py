@@ -62,8 +62,8 @@ _gemm_forced_splits = 0   # tools/gemm_splits.py probe: forces the split count o
 # accumulating / in-place epilogues are not disturbed) and caches the fastest; later launches use
 # otamd_gemm_explicit.  Candidate plans all compute the same product; they differ only in the fp32
 # summation order of split-K.
-_TUNE = {"on": False, "cache": {}, "reps": 3}
-_TILES = (0, 1, 2, 3, 4, 5, 6, -1)
+_TUNE = {"on": False, "cache": {}, "reps": int(os.environ.get("OTAMD_TUNE_REPS", "3"))}
+_TILES = tuple(int(t) for t in os.environ.get("OTAMD_TUNE_TILES", "0,1,2,3,4,5,6,7,8,-1").split(","))
 _SPLITS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 16)
 
 
@@ -119,6 +119,52 @@ def _tune(a: GemmArgs, device) -> tuple:
     return best
 
 
+# ---- measured plan table --------------------------------------------------------------------
+# (tile, split-K) per GEMM signature, timed on MI355X by the autotuner above inside the real train steps
+# of the benchmarked configurations (bench.py --autotune --dump-plans; tools/gpu_plans.sh) and committed
+# as data: deterministic plans (the same split-K summation order in every process, so resume stays
+# bit-exact), measured rather than modelled.  Signatures not in the table use the analytic plan.
+# OTAMD_GEMM_TABLE=0 disables it (A/B against the analytic planner).
+_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plans_mi355x.json")
+_PLAN_TABLE = None
+
+
+def _plan_table() -> dict:
+    global _PLAN_TABLE
+    if _PLAN_TABLE is None:
+        _PLAN_TABLE = {}
+        if os.environ.get("OTAMD_GEMM_TABLE", "1") != "0" and os.path.exists(_TABLE_PATH):
+            import json
+            with open(_TABLE_PATH) as f:
+                for row in json.load(f)["plans"]:
+                    _PLAN_TABLE[tuple(row["key"])] = (int(row["tile"]), int(row["splits"]))
+    return _PLAN_TABLE
+
+
+def plan_source() -> str:
+    n = len(_plan_table())
+    return f"measured plan table ({n} signatures, {os.path.basename(_TABLE_PATH)}) + analytic" if n else "analytic"
+
+
+def dump_plan_table(path: str, merge: bool = True) -> int:
+    """write the autotuner's cache as a plan table (merged into an existing file at `path`)."""
+    import json
+    rows = {}
+    if merge and os.path.exists(path):
+        with open(path) as f:
+            for row in json.load(f)["plans"]:
+                rows[tuple(row["key"])] = row
+    for key, (t, sp) in _TUNE["cache"].items():
+        rows[tuple(int(x) for x in key)] = {"key": [int(x) for x in key], "tile": int(t), "splits": int(sp)}
+    out = {"device": "MI355X (gfx950)",
+           "key": "amode, bmode, M, N, K, K1, batch, c_f32, bias, rowvec, residual, accumulate, ga.KH, ga.stride, "
+                  "ga.upsample, gb.KH",
+           "plans": sorted(rows.values(), key=lambda r: r["key"])}
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0)
+    return len(rows)
+
+
 def _plan_overrides() -> dict:
     """OTAMD_GEMM_PLAN="am,bm,M,N,K:tile:splits;..." pins the (tile, split-K) of listed GEMM shapes
     (A/B measurements of planner changes inside the real step)."""
@@ -149,11 +195,15 @@ def _gemm(a: GemmArgs, splits: int, device) -> None:
             return
     if splits == 0 and _gemm_forced_splits:
         splits = _gemm_forced_splits
+    plan = None
     if splits == 0 and _TUNE["on"]:
         key = _tune_key(a)
         plan = _TUNE["cache"].get(key)
         if plan is None:
             plan = _TUNE["cache"][key] = _tune(a, device)
+    elif splits == 0:
+        plan = _plan_table().get(_tune_key(a))
+    if plan is not None:
         t, s = plan
         ws_bytes = s * a.M * a.N * 4 if s > 1 else 0
         ws = workspace(ws_bytes, device) if ws_bytes else None

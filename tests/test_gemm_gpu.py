@@ -138,9 +138,10 @@ def test_autotuned_plans(dev, autotune):
     assert len(K.gemm_autotune_cache()) == n
 
 
-@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_every_tile_explicit(dev, tile, monkeypatch):
-    """every engine tile (4 = 128x128 with 8 waves, 2 workgroups per CU; 5 / 6 = 128x64 / 64x128) through otamd_gemm_explicit:
+    """every engine tile (4 = 128x128 with 8 waves, 2 workgroups per CU; 5 / 6 = 128x64 / 64x128; 7 / 8 = 128x160 /
+    256x160, 20 DMA pieces over 8 waves and 320-byte MN rows) through otamd_gemm_explicit:
     linear fwd (+bias +residual), dgrad, wgrad (split-K) and conv fwd / dgrad / wgrad, ragged sizes."""
     torch.manual_seed(11)
     splits = {"v": 1}

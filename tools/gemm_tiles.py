@@ -86,7 +86,7 @@ def main():
                 continue
             ws_bytes = se * a.M * a.N * 4 if se > 1 else 0
             ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
-            for t in (0, 1, 2, 3, 4, -1) + ((5,) if se == 1 else ()):   # 5: coop split-K, all CUs
+            for t in (0, 1, 2, 4, 7, 8):
                 rc = lib.otamd_gemm_explicit(C.byref(a), t, se, ws.data_ptr(), ws_bytes, K.stream_handle())
                 if rc != 0:
                     continue
