@@ -15,6 +15,7 @@ start()/train()/end() keep the reference's external behaviour (scripts/train.py:
 """
 from __future__ import annotations
 
+import gc
 import time
 
 import torch
@@ -203,7 +204,14 @@ class GenericTrainer:
                 loss = self.train_step(batch)
                 self.loss_history.append(loss)
                 steps += 1
+                if steps == 1:
+                    # long-lived objects (model, plans, workspaces) out of the collector's generations; cyclic GC
+                    # then runs only at the log points below, not as a pause inside a step's kernel issue
+                    gc.collect()
+                    gc.freeze()
+                    gc.disable()
                 if log_every and steps % log_every == 0:
+                    gc.collect()
                     vals = torch.stack(self.loss_history[-log_every:]).float()
                     if self.world > 1:
                         torch.distributed.all_reduce(vals)
@@ -211,10 +219,13 @@ class GenericTrainer:
                     if self.rank == 0:
                         print(f"step {tp.global_step}: loss {vals.mean().item():.5f}", flush=True)
                 if self.commands is not None and getattr(self.commands, "get_stop_command", lambda: False)():
+                    gc.enable()
                     return
                 if max_steps is not None and steps >= max_steps:
+                    gc.enable()
                     return
             tp.next_epoch()
+        gc.enable()
 
     def end(self):
         if torch.cuda.is_available():

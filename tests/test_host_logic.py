@@ -146,3 +146,19 @@ def test_flux_lora_groups():
     assert full.site_of["transformer_blocks.0.norm1.linear"].group == (
         "transformer_blocks.0.norm1.linear", "transformer_blocks.0.norm1_context.linear")
     del torch
+
+
+def test_gemm_plan_table_wellformed():
+    """the committed measured plan table (onetrainer_amd/gemm_plans_mi355x.json): every row a full
+    signature key with a valid (tile, split-K) plan; loaded by kernels._plan_table."""
+    import json
+    from onetrainer_amd import kernels as K
+    with open(K._TABLE_PATH) as f:
+        rows = json.load(f)["plans"]
+    assert len(rows) > 100
+    for r in rows:
+        assert len(r["key"]) == 16 and r["key"][2] > 0 and r["key"][3] > 0 and r["key"][4] > 0
+        assert -1 <= r["tile"] <= 8 and r["splits"] >= 1
+        if r["key"][1] == 5 or r["key"][5]:   # conv-weight B / second K segment: v2 tiles only
+            assert r["tile"] >= 0
+    assert len(K._plan_table()) == len({tuple(r["key"]) for r in rows})
