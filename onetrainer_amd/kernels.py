@@ -22,8 +22,12 @@ F32 = torch.float32
 OPM_K, OPM_MN, OPM_CONV_FWD, OPM_CONV_DGRAD, OPM_CONV_WGRAD, OPM_CONV_WT = 0, 1, 2, 3, 4, 5
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream   # C calls: torch.cuda.current_stream() builds a Python
+_cur_device = torch._C._cuda_getDevice              # Stream object per launch (~8 us of host time each)
+
+
 def stream_handle() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _raw_stream(_cur_device())
 
 
 def _p(t: torch.Tensor | None) -> int | None:
@@ -44,8 +48,8 @@ def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     """scratch for the launch about to be queued on the current stream: one buffer per
     (device, stream), so work on the weight-gradient side stream (module/streams.py) never shares
     split-K slabs with the main stream.  Reuse is stream-ordered."""
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
+    idx = device.index if device.index is not None else _cur_device()
+    key = (idx, _raw_stream(idx))
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(max(nbytes, 64 << 20), dtype=torch.uint8, device=device)

@@ -26,8 +26,24 @@ _SIDE: dict = {}
 _ENABLED = os.environ.get("OTAMD_WGRAD_STREAM", "1") != "0"
 
 
+_AVAIL = None
+_STREAMS: dict = {}   # raw HIP stream -> torch Stream object (current_stream() builds a new one per call)
+_EVENTS: dict = {}    # side stream index -> reusable fork event (a wait captures the record current at enqueue)
+
+
 def enabled() -> bool:
-    return _ENABLED and torch.cuda.is_available()
+    global _AVAIL
+    if _AVAIL is None:
+        _AVAIL = torch.cuda.is_available()
+    return _ENABLED and _AVAIL
+
+
+def _current(idx: int):
+    raw = torch._C._cuda_getCurrentRawStream(idx)
+    st = _STREAMS.get(raw)
+    if st is None:
+        st = _STREAMS[raw] = torch.cuda.current_stream(idx)
+    return st
 
 
 def set_enabled(on: bool):
@@ -38,9 +54,9 @@ def set_enabled(on: bool):
 def side_stream(device=None):
     if not enabled():
         return None
-    idx = torch.cuda.current_device() if device is None else torch.device(device).index
+    idx = torch._C._cuda_getDevice() if device is None else torch.device(device).index
     if idx is None:
-        idx = torch.cuda.current_device()
+        idx = torch._C._cuda_getDevice()
     s = _SIDE.get(idx)
     if s is None:
         s = torch.cuda.Stream(device=idx)
@@ -54,10 +70,18 @@ def wgrad_region(tensors=()):
     if side is None:
         yield
         return
-    main = torch.cuda.current_stream()
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
+    idx = side.device_index
+    main = _current(idx)
+    ev = _EVENTS.get(idx)
+    if ev is None:
+        ev = _EVENTS[idx] = torch.cuda.Event()
+    ev.record(main)
+    side.wait_event(ev)
+    torch.cuda.set_stream(side)
+    try:
         yield
+    finally:
+        torch.cuda.set_stream(main)
     for t in tensors:
         if t is not None and t.is_cuda:
             t.record_stream(side)

@@ -31,3 +31,14 @@ for i in range(5):
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"step {i}: host issue {1e3 * (t1 - t0):.1f} ms, wall {1e3 * (t2 - t0):.1f} ms", flush=True)
+if os.environ.get("HO_PROFILE", "0") == "1":   # where the host issue time goes (cProfile, one step)
+    import cProfile
+    import pstats
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    with torch.autograd.set_multithreading_enabled(False):   # backward's Python on this thread (profiled)
+        pr.enable()
+        tr.train_step(batch)
+        pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(45)
