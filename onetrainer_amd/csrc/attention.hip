@@ -456,8 +456,10 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 // CU to one block, so the full 512-entry register file is used instead of spilling at 256.
 // (A software-pipelined D = 128 variant -- S / dP of tile t+1 on the MFMA pipe during tile t's
 // softmax, 4-deep ring -- measured slower: 1487-1510 vs 1349 us for the Flux bwd; not kept.)
-template <int D>
-__global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(AttnArgs a) {
+// OCC = waves per SIMD.  D = 64 at OCC = 3 (<= 168 VGPRs: the tile loop not unrolled) fits 768 blocks on
+// the chip, the SDXL level-2 grid (8 key blocks x 20 heads x 4 = 640) in one round instead of 1.25 at OCC 2.
+template <int D, int OCC = 1>
+__global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = QT * D * 2;                 // one [32 x D] image
   constexpr int STG = 4 * TB + QT * 8;           // + 32 float2 pairs
@@ -575,7 +577,7 @@ __global__ void __launch_bounds__(256, D <= 64 ? 2 : 1) attn_bwd_dkv_kernel(Attn
     softmax_pack(S, dP, st, pk);
     dvdk(st, pk);
   };
-  stage_loop<NS, (D <= 64)>(ntiles, step);
+  stage_loop<NS, (D <= 64 && OCC < 3)>(ntiles, step);
   const int key = k0 + r;
   if (key < a.Nk) {
 #pragma unroll
@@ -708,7 +710,7 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   dim3 gk(kblocks, a.H, a.B * qsplit);
   if (a.Dv <= 64) {
     launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
-    launch(attn_bwd_dkv_kernel<64>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);
+    launch(attn_bwd_dkv_kernel<64, 3>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);   // SDXL bwd 17.18 -> 16.71 ms/step
   } else {
     launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // bwd 1349 vs 1467 us (64-key tiles)
     launch(attn_bwd_dkv_kernel<128>, gk, 3 * (4 * QT * 128 * 2 + QT * 8), stream, a);

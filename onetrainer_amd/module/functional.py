@@ -109,6 +109,39 @@ class LinearFn(torch.autograd.Function):
         return (dx, None, None, dres) + (None,) * (len(ctx.needs_input_grad) - 4)
 
 
+class PrecomputedLinearFn(torch.autograd.Function):
+    """y = x W^T whose forward was computed already (one batched GEMM with its sibling layers, see
+    UNet2DConditionModel._kv_batched); holder = [y].  Backward is LinearFn's (no bias / residual):
+    weight gradient on the side stream, dx only when x needs it."""
+
+    @staticmethod
+    def forward(ctx, x, wref, holder, *params):
+        x2 = _rows(x)
+        ctx.save_for_backward(x2)
+        ctx.wref, ctx.xshape = wref, x.shape
+        y = holder[0]
+        return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x2,) = ctx.saved_tensors
+        wref = ctx.wref
+        dy2 = _rows(dy)
+        if dy2.stride(1) != 1 or dy2.stride(0) % 8:
+            dy2 = dy2.contiguous()
+        if wref.trainable:
+            with S.wgrad_region((dy2, x2)):
+                K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
+        dx = K.linear_dgrad(dy2, wref.w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        if wref.trainable:
+            wref.done()
+        return (dx, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
+
+
+def precomputed_linear(x, wref, y):
+    return PrecomputedLinearFn.apply(x, wref, [y], *_params(wref))
+
+
 def linear(x, wref, bref=None, residual=None, lora=None):
     if lora is not None:
         return LoraLinearFn.apply(x, wref, bref, residual, lora, *lora.params, *_trainable_params(wref, bref))
