@@ -9,4 +9,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_${TAG}_$C -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-vae > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { echo "pmc pass $C failed"; tail -20 gpurun_out/pmc_${TAG}_$C.log; exit 1; }
   find gpurun_out/pmc_${TAG}_$C -name '*.csv' | head
 done
-python3 tools/pmc_traffic.py gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE > gpurun_out/pmc_${TAG}.json && cat gpurun_out/pmc_${TAG}.json
+python3 tools/pmc_traffic.py gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE > gpurun_out/pmc_${TAG}.json && rm -rf gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE && cat gpurun_out/pmc_${TAG}.json

@@ -41,6 +41,17 @@ def main():
     union += ce - cs
     print(f"  union busy {union / 1e6:.2f} ms; idle {span - union / 1e6:.2f} ms in {len(gaps)} gaps "
           f"(>10us: {sum(1 for g in gaps if g > 10000)}, total {sum(g for g in gaps if g > 10000) / 1e6:.2f} ms)")
+    # the backward's tail: main-stream idle between its last kernel before the grad-norm (the join) and
+    # the grad-norm launch, i.e. time the main stream waits for the weight-gradient side stream
+    gn = [r for r in step if "grad_sqnorm" in r[0]]
+    if gn:
+        g0 = gn[0][3]
+        main_key = max(by_stream, key=lambda k: len(by_stream[k]))
+        before = [r for r in by_stream[main_key] if r[4] <= g0 and r is not gn[0]]
+        side = [r for k, v in by_stream.items() if k != main_key for r in v if r[4] <= g0]
+        if before and side:
+            print(f"  join: main idle {(g0 - max(r[4] for r in before)) / 1e6:.2f} ms before the grad norm; "
+                  f"side stream ends {(max(r[4] for r in side) - max(r[4] for r in before)) / 1e6:.2f} ms after main's last kernel")
     for k, v in by_stream.items():
         agg = collections.Counter()
         for r in v:
