@@ -428,14 +428,16 @@ class SelfAttnFn(torch.autograd.Function):
 
 
 class CrossAttnFn(torch.autograd.Function):
-    """q [B, N, C], kv [B, L, 2C] -> o [B, N, C]."""
+    """q [B, N, C], kv [B, L, 2C] -> o [B, N, C].  kv_side: kv's gradient feeds only a weight gradient on the
+    side stream (the K/V projection of frozen text states, PrecomputedLinearFn), so dK / dV are computed
+    there too and the main stream goes on with dQ."""
 
     @staticmethod
-    def forward(ctx, q, kv, heads):
+    def forward(ctx, q, kv, heads, kv_side=False):
         C = q.shape[-1]
         o, lse = K.attn_fwd(q, kv[..., :C], kv[..., C:], heads)
         ctx.save_for_backward(q, kv, o, lse)
-        ctx.heads = heads
+        ctx.heads, ctx.kv_side = heads, kv_side
         return o
 
     @staticmethod
@@ -445,8 +447,10 @@ class CrossAttnFn(torch.autograd.Function):
         C = q.shape[-1]
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
-        K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:])
-        return dq, (dkv if ctx.needs_input_grad[1] else None), None
+        side = S.side_stream() if ctx.kv_side and ctx.needs_input_grad[1] else None
+        K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:],
+                   kv_stream=side)
+        return dq, (dkv if ctx.needs_input_grad[1] else None), None, None
 
 
 class GEGLUFn(torch.autograd.Function):
