@@ -116,10 +116,6 @@ int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream);
 /* replaces: autograd of scaled_dot_product_attention (GenericTrainer.py:693-696) */
 int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream);
 
-/* replaces: the same backward in two parts (parts & 1: dQ + the {lse, delta} pairs; parts & 2: dK/dV, after
-   part 1), each on the caller's stream: cross-attention's dK/dV run on the weight-gradient stream */
-int otamd_attn_bwd_part(const AttnArgs* in, float* ws, long long ws_bytes, int parts, hipStream_t stream);
-
 /* workspace bytes otamd_attn_bwd needs for these arguments ({lse, delta} pairs + split-query partials) */
 long long otamd_attn_bwd_ws_bytes(const AttnArgs* in);
 

@@ -101,7 +101,6 @@ SIGNATURES: dict[str, list] = {
     "otamd_attn_args_size": [],
     "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],
     "otamd_attn_bwd": [C.POINTER(AttnArgs), VP, LL, VP],
-    "otamd_attn_bwd_part": [C.POINTER(AttnArgs), VP, LL, I, VP],
     "otamd_attn_bwd_ws_bytes": [C.POINTER(AttnArgs)],
     # softmax.hip (materialized attention for heads > 128)
     "otamd_softmax_rows_fwd": [VP, LL, VP, LL, VP, LL, I, I, F, VP],

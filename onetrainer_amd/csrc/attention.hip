@@ -687,23 +687,8 @@ OTAMD_API long long otamd_attn_bwd_ws_bytes(const AttnArgs* in) {
   return nrow * 8 + 256 + (qs > 1 ? 2LL * qs * nkv * 4 : 0);
 }
 
-static int attn_bwd_impl(const AttnArgs* in, float* ws, long long ws_bytes, int parts, hipStream_t stream);
-
 // ws: otamd_attn_bwd_ws_bytes(args) bytes, 16-byte aligned; lse from the forward
 OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream) {
-  return attn_bwd_impl(in, ws, ws_bytes, 3, stream);
-}
-
-// the backward in two parts on the caller's streams: parts & 1 = dQ (+ the {lse, delta} pairs into ws),
-// parts & 2 = dK / dV (+ the split-query cast), which reads those pairs: order it after part 1 (an event).
-// Cross-attention's dK / dV feed only the K/V projection's weight gradient, so the caller queues part 2
-// on its weight-gradient stream and the dQ chain continues without it.
-OTAMD_API int otamd_attn_bwd_part(const AttnArgs* in, float* ws, long long ws_bytes, int parts, hipStream_t stream) {
-  if (parts < 1 || parts > 3) return OTAMD_EINVAL;
-  return attn_bwd_impl(in, ws, ws_bytes, parts, stream);
-}
-
-static int attn_bwd_impl(const AttnArgs* in, float* ws, long long ws_bytes, int parts, hipStream_t stream) {
   if (!in || !attn_ok(*in) || !in->o || !in->lse || !in->dout || !in->dq || !in->dk || !in->dv || !ws) return OTAMD_EINVAL;
   AttnArgs a = *in;
   if (a.lddo % 8 || a.bsdo % 8 || a.lddq % 8 || a.lddk % 8 || a.lddv % 8 || a.bsdq % 8 || a.bsdk % 8 || a.bsdv % 8 ||
@@ -724,14 +709,14 @@ static int attn_bwd_impl(const AttnArgs* in, float* ws, long long ws_bytes, int 
   dim3 gq((a.Nq + 127) / 128, a.H, a.B);
   dim3 gk(kblocks, a.H, a.B * qsplit);
   if (a.Dv <= 64) {
-    if (parts & 1) launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
-    if (parts & 2) launch(attn_bwd_dkv_kernel<64, 3>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);   // SDXL bwd 17.18 -> 16.71 ms/step
+    launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
+    launch(attn_bwd_dkv_kernel<64, 3>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);   // SDXL bwd 17.18 -> 16.71 ms/step
   } else {
-    if (parts & 1) launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // bwd 1349 vs 1467 us (64-key tiles)
-    if (parts & 2) launch(attn_bwd_dkv_kernel<128>, gk, 3 * (4 * QT * 128 * 2 + QT * 8), stream, a);
+    launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // bwd 1349 vs 1467 us (64-key tiles)
+    launch(attn_bwd_dkv_kernel<128>, gk, 3 * (4 * QT * 128 * 2 + QT * 8), stream, a);
   }
   OTAMD_CHECK_LAUNCH();
-  if (qsplit > 1 && (parts & 2)) {
+  if (qsplit > 1) {
     int blocks = (int)std::min<long long>((nkv / 4 + 255) / 256, 8192);
     attn_dkv_cast_kernel<<<blocks, 256, 0, stream>>>(a);
     OTAMD_CHECK_LAUNCH();

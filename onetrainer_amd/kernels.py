@@ -756,11 +756,8 @@ def attn_fwd(q, k, v, heads, scale=None, out=None):
     return out, lse
 
 
-def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None, kv_stream=None):
-    """flash-attention backward; kv_stream: queue dK / dV there (after dQ), e.g. the weight-gradient stream
-    when only a weight gradient consumes them (cross-attention: the K/V projection of frozen text states)."""
+def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None):
     if q.shape[-1] // heads > FLASH_MAX_D:
-        kv_stream = None   # materialized path: one stream
         return attn_mat_bwd(q, k, v, lse, dout, heads, scale, dq, dk, dv)
     a = _attn_args(q, k, v, heads, scale)
     dq = torch.empty(q.shape, dtype=BF16, device=q.device) if dq is None else dq
@@ -775,19 +772,8 @@ def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None
     a.lddv, a.bsdv = _attn_view(dv, heads)
     nbytes = lib().otamd_attn_bwd_ws_bytes(C.byref(a))
     _req(nbytes > 0, "attention workspace query")
-    if kv_stream is None:
-        ws = workspace(nbytes, q.device)
-        check(lib().otamd_attn_bwd(C.byref(a), _p(ws), nbytes, stream_handle()), "otamd_attn_bwd")
-        return dq, dk, dv
-    # dQ here, dK / dV on kv_stream after it; the workspace (the {lse, delta} pairs part 2 reads) is a
-    # private allocation that the caching allocator keeps until kv_stream has used it
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=q.device)
-    check(lib().otamd_attn_bwd_part(C.byref(a), _p(ws), nbytes, 1, stream_handle()), "otamd_attn_bwd_part")
-    main = torch.cuda.current_stream(q.device)
-    kv_stream.wait_stream(main)
-    check(lib().otamd_attn_bwd_part(C.byref(a), _p(ws), nbytes, 2, kv_stream.cuda_stream), "otamd_attn_bwd_part")
-    for t in (ws, q, k, v, o, lse, dout, dk, dv):
-        t.record_stream(kv_stream)
+    ws = workspace(nbytes, q.device)
+    check(lib().otamd_attn_bwd(C.byref(a), _p(ws), nbytes, stream_handle()), "otamd_attn_bwd")
     return dq, dk, dv
 
 

@@ -428,16 +428,14 @@ class SelfAttnFn(torch.autograd.Function):
 
 
 class CrossAttnFn(torch.autograd.Function):
-    """q [B, N, C], kv [B, L, 2C] -> o [B, N, C].  kv_side: kv's gradient feeds only a weight gradient on the
-    side stream (the K/V projection of frozen text states, PrecomputedLinearFn), so dK / dV are computed
-    there too and the main stream goes on with dQ."""
+    """q [B, N, C], kv [B, L, 2C] -> o [B, N, C]."""
 
     @staticmethod
-    def forward(ctx, q, kv, heads, kv_side=False):
+    def forward(ctx, q, kv, heads):
         C = q.shape[-1]
         o, lse = K.attn_fwd(q, kv[..., :C], kv[..., C:], heads)
         ctx.save_for_backward(q, kv, o, lse)
-        ctx.heads, ctx.kv_side = heads, kv_side
+        ctx.heads = heads
         return o
 
     @staticmethod
@@ -447,10 +445,8 @@ class CrossAttnFn(torch.autograd.Function):
         C = q.shape[-1]
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
-        side = S.side_stream() if ctx.kv_side and ctx.needs_input_grad[1] else None
-        K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:],
-                   kv_stream=side)
-        return dq, (dkv if ctx.needs_input_grad[1] else None), None, None
+        K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:])
+        return dq, (dkv if ctx.needs_input_grad[1] else None), None
 
 
 class GEGLUFn(torch.autograd.Function):

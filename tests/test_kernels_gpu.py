@@ -152,23 +152,6 @@ def test_attention_strided_qkv(dev):
     assert rel_err(o, ref) < 2e-2
 
 
-@pytest.mark.parametrize("Nq,Nk", [(1024, 77), (4096, 77), (1024, 1024)])
-def test_attention_backward_in_two_streams(dev, Nq, Nk):
-    """otamd_attn_bwd_part: dQ on the current stream, dK / dV queued on a second stream after it (how the
-    cross-attention backward runs): bit-identical to the one-stream backward."""
-    torch.manual_seed(13)
-    B, H, D = 2, 4, 64
-    q, k, v = rnd(B, Nq, H * D, dev=dev), rnd(B, Nk, H * D, dev=dev), rnd(B, Nk, H * D, dev=dev)
-    o, lse = K.attn_fwd(q, k, v, H)
-    do = rnd(B, Nq, H * D, dev=dev)
-    ref = K.attn_bwd(q, k, v, o, lse, do, H)
-    side = torch.cuda.Stream(device=dev)
-    dq, dk, dv = K.attn_bwd(q, k, v, o, lse, do, H, kv_stream=side)
-    torch.cuda.current_stream().wait_stream(side)
-    for x, y in zip((dq, dk, dv), ref):
-        assert torch.equal(x, y)
-
-
 def test_geglu(dev):
     torch.manual_seed(4)
     h = rnd(300, 2 * 2560, dev=dev)
