@@ -257,6 +257,7 @@ def main():
     gc.collect()
     gc.freeze()
     gc.disable()
+    ms0 = torch.cuda.memory_stats(dev)
     t_start = time.perf_counter()
     evs[0].record(stream)
     losses = []
@@ -269,6 +270,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     gc.enable()
+    ms1 = torch.cuda.memory_stats(dev)
+    alloc = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries",
+                                                          "num_sync_all_streams")}
     step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     p50 = step_ms[len(step_ms) // 2]
     p90 = step_ms[min(len(step_ms) - 1, int(0.9 * len(step_ms)))]
@@ -337,6 +341,7 @@ def main():
         "step_ms_p50": round(p50, 2),
         "step_ms_p90": round(p90, 2),
         "step_ms_max": round(step_ms[-1], 2),
+        "allocator_in_timed_steps": alloc,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
