@@ -216,6 +216,20 @@ __device__ __forceinline__ void splitk_combine(const GemmArgs& args, unsigned m,
     }
 #pragma unroll
   for (int t = 0; t < V; ++t) v[t] *= args.alpha;
+  if constexpr (V == 8) {   // 16-byte epilogue operands (one load each instead of 8 two-byte loads)
+    if (gemm_wide_ok(args) && !args.c_f32) {
+      float w[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) w[t] = v[t];
+      if (args.bias) add_bf8(w, *reinterpret_cast<const uint4*>(args.bias + n));
+      if (args.rowvec) add_bf8(w, *reinterpret_cast<const uint4*>(args.rowvec + (long long)(m / args.rows_per_vec) * args.ldv + n));
+      if (args.residual) add_bf8(w, *reinterpret_cast<const uint4*>(args.residual + (long long)m * args.ldr + n));
+      bf16_t* dst = reinterpret_cast<bf16_t*>(args.C) + (long long)m * args.ldc + n;
+      if (args.accumulate) add_bf8(w, *reinterpret_cast<const uint4*>(dst));
+      *reinterpret_cast<bf8*>(dst) = pack8(w);
+      return;
+    }
+  }
   if (args.bias)
 #pragma unroll
     for (int t = 0; t < V; ++t) v[t] += bf2f(args.bias[n + t]);
