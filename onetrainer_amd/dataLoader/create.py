@@ -135,11 +135,13 @@ def build_cache(config, model, device, rank: int = 0) -> int:
     if fam == "sdxl":
         text_fn = lambda t: TE.encode_sdxl_text(model.text_encoder_1, model.text_encoder_2,  # noqa: E731
                                                 t["tokens_1"], t["tokens_2"])
-        rows = [{"image": Image.open(p), "tokens": {"tokens_1": ids(toks[0], c), "tokens_2": ids(toks[1], c)}}
-                for p, c in samples]
+        rows = ({"image": Image.open(p), "tokens": {"tokens_1": ids(toks[0], c), "tokens_2": ids(toks[1], c)}}
+                for p, c in samples)
     else:
         text_fn = lambda t: TE.encode_sd15_text(model.text_encoder_1, t["tokens_1"])  # noqa: E731
-        rows = [{"image": Image.open(p), "tokens": {"tokens_1": ids(toks[0], c)}} for p, c in samples]
+        rows = ({"image": Image.open(p), "tokens": {"tokens_1": ids(toks[0], c)}} for p, c in samples)
+    # a generator: each file is opened (and, once decoded, closed) inside the writer's loop, so a concept
+    # folder larger than the open-file limit caches
     writer = LatentCacheWriter(lambda im: model.vae_encoder.encode(im), cfg.cache_dir, default_bucketing(cfg),
                                device, rank=rank, text_fn=text_fn)
     return writer.write(rows)

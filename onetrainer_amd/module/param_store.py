@@ -49,13 +49,13 @@ class FlatParamStore:
         self.trainable = trainable
         self.data = torch.zeros(self.numel, dtype=dtype, device=device)
         self.grad = torch.zeros(self.numel, dtype=dtype, device=device) if trainable else None
-        self.params: dict[str, torch.nn.Parameter] = {}
+        self._params: dict[str, torch.nn.Parameter] = {}
         for name in self.order:
             s = self.slots[name]
             p = torch.nn.Parameter(self.data[s.offset:s.offset + s.numel].view(s.shape), requires_grad=trainable)
             if trainable:
                 p.grad = self.grad[s.offset:s.offset + s.numel].view(s.shape)
-            self.params[name] = p
+            self._params[name] = p
         self._written: set[str] = set()
         self.accumulating = False          # True on micro-steps after the first of a GA window
         self.ready_hooks = []              # callables(names) -> None (DP reducer)
@@ -65,8 +65,18 @@ class FlatParamStore:
         self._waited = 0
 
     # ----- views -------------------------------------------------------------------------------
+    @property
+    def params(self) -> dict:
+        """name -> parameter view.  A reader that takes weights from here (or from view()) rather than
+        through PRef.w is ordered after an optimizer update still in flight on its own stream
+        (util/optimizer/adamw_fused.py overlap): it waits for every pending chunk."""
+        if self.update_events is not None:
+            self.wait_params()
+        return self._params
+
     def view(self, names, shape=None, grad=False):
-        """contiguous view spanning `names` (which must be adjacent without padding)."""
+        """contiguous view spanning `names` (which must be adjacent without padding); a weight view
+        waits for the optimizer chunks covering it when an update is in flight."""
         if isinstance(names, str):
             names = [names]
         first = self.slots[names[0]]
@@ -79,6 +89,8 @@ class FlatParamStore:
         buf = self.grad if grad else self.data
         if buf is None:
             return None
+        if not grad and self.update_events is not None:
+            self.wait_params(end)
         v = buf[first.offset:end]
         if shape is not None:
             v = v.view(shape)
@@ -140,7 +152,7 @@ class FlatParamStore:
                     self.grad[s.offset:s.offset + s.numel].zero_()
 
     def named_parameters(self):
-        return [(n, self.params[n]) for n in self.order]
+        return [(n, self._params[n]) for n in self.order]
 
     def group_ranges(self):
         """{group: (begin, end)} element ranges; groups must be contiguous in layout order."""

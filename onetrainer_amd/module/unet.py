@@ -86,6 +86,37 @@ def tiny_sd15_config() -> UNetConfig:
                       addition_embed=False, norm_num_groups=32)
 
 
+def unet_config_from_diffusers(d: dict) -> UNetConfig:
+    """UNet2DConditionModel config.json (what diffusers' from_pretrained builds the architecture from,
+    HFModelLoaderMixin.py:61-101) -> UNetConfig.  diffusers' `attention_head_dim` is the head COUNT
+    per block (int or list); equal head widths become `head_dim`, else a fixed head count."""
+    chans = tuple(d["block_out_channels"])
+    n = len(chans)
+    heads = d.get("num_attention_heads") or d.get("attention_head_dim", 8)
+    heads = list(heads) if isinstance(heads, (list, tuple)) else [heads] * n
+    widths = {c // h for c, h in zip(chans, heads)}
+    tl = d.get("transformer_layers_per_block", 1)
+    tl = tuple(tl) if isinstance(tl, (list, tuple)) else (tl,) * n
+    down = tuple(d["down_block_types"])
+    add = d.get("addition_embed_type") == "text_time"
+    kw = dict(in_channels=d.get("in_channels", 4), out_channels=d.get("out_channels", 4), block_out_channels=chans,
+              down_block_types=down, up_block_types=tuple(d["up_block_types"]),
+              layers_per_block=d.get("layers_per_block", 2), transformer_layers_per_block=tl,
+              cross_attention_dim=d.get("cross_attention_dim", 1280),
+              use_linear_projection=bool(d.get("use_linear_projection", False)), addition_embed=add,
+              norm_num_groups=d.get("norm_num_groups", 32), norm_eps=d.get("norm_eps", 1e-5))
+    if len(widths) == 1:
+        kw.update(head_dim=widths.pop(), num_heads=None)
+    elif len(set(heads)) == 1:
+        kw.update(head_dim=None, num_heads=heads[0])
+    else:
+        raise NotImplementedError(f"per-block head counts {heads} with differing head widths")
+    if add:
+        kw.update(addition_time_embed_dim=d.get("addition_time_embed_dim", 256),
+                  projection_class_embeddings_input_dim=d.get("projection_class_embeddings_input_dim", 2816))
+    return UNetConfig(**kw)
+
+
 PAD_IN = 8    # conv_in input channels held (latent channels zero-padded)
 PAD_OUT = 8   # conv_out output channels held
 

@@ -23,16 +23,19 @@ import torch
 from ..util import create
 from ..util.config.plain import plain
 from ..util.lr_scheduler_util import create_lr_scheduler
+from ..util.TimedActionMixin import TimedActionMixin
+from ..util.TrainCommands import TrainCommands
 from ..util.TrainProgress import TrainProgress
 from .ddp import GradBucketReducer, init_from_env
 
 
-class GenericTrainer:
+class GenericTrainer(TimedActionMixin):
     def __init__(self, config, callbacks=None, commands=None, model=None, model_setup=None, data_loader=None,
                  seed=0):
+        super().__init__()
         self.config = plain(config)       # the reference's enum-typed TrainConfig or this build's
         self.callbacks = callbacks
-        self.commands = commands
+        self.commands = commands if commands is not None else TrainCommands()
         self.model = model
         self.model_setup = model_setup
         self.data_loader = data_loader
@@ -41,6 +44,10 @@ class GenericTrainer:
         self.reducer = None
         self.graphs = None
         self.loss_history: list[torch.Tensor] = []
+        self.one_step_trained = False
+        self._has_gradient = False
+        self._wallclock_timers = False
+        self.rank, self.world = 0, 1
 
     # ------------------------------------------------------------------------------------------
     def start(self):
@@ -144,19 +151,57 @@ class GenericTrainer:
             for d in dirs[keep:]:
                 shutil.rmtree(os.path.join(root, d), ignore_errors=True)
 
-    def save(self, destination: str | None = None, output_format: str | None = None, dtype=None) -> str:
-        """final model (GenericTrainer.py:752-790): config.output_model_destination / _format."""
+    def save(self, train_progress: TrainProgress | None = None, print_msg: bool = True, print_cb=print) -> str | None:
+        """periodic save (GenericTrainer.py:453-497) to <workspace>/save/<prefix><timestamp>-save-
+        <global_step>-<epoch>-<epoch_step><ext> in output_model_format / output_dtype; rank 0 writes,
+        a failed save is reported and its partial output removed."""
+        import os
+        from datetime import datetime
+        cfg = self.config
+        tp = train_progress or self.model.train_progress
+        path = os.path.join(cfg.workspace_dir, "save",
+                            f"{cfg.save_filename_prefix}{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}-save-"
+                            f"{tp.filename_string()}{_file_extension(cfg.output_model_format)}")
+        if print_msg and self.rank == 0:
+            print_cb("Saving " + path)
+        return self._write_model(path, cfg.output_model_format)
+
+    def _write_model(self, path: str, fmt: str) -> str | None:
+        import os
+        import shutil
+        import traceback
+
         from ..modelSaver import create_model_saver
         cfg = self.config
-        dest = destination or cfg.output_model_destination
+        ok = True
         if self.rank == 0:
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-            create_model_saver(cfg.model_type, cfg.training_method).save(self.model, cfg,
-                                                                          output_format or cfg.output_model_format,
-                                                                          dest, dtype)
+            try:
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+                create_model_saver(cfg.model_type, cfg.training_method).save(self.model, cfg, fmt, path,
+                                                                              _torch_dtype(cfg.output_dtype))
+            except Exception:
+                traceback.print_exc()
+                print("Could not save model. Check your disk space!")
+                ok = False
+                if os.path.isdir(path):
+                    shutil.rmtree(path, ignore_errors=True)
+                elif os.path.isfile(path):
+                    os.remove(path)
         if self.world > 1:
             torch.distributed.barrier()
+        return path if ok else None
+
+    def final_model_path(self) -> str:
+        """end()'s destination (GenericTrainer.py:778-785): a single-file format into an existing
+        directory gets a timestamped file name inside it."""
+        import os
+        from datetime import datetime
+        cfg = self.config
+        dest = cfg.output_model_destination
+        ext = _file_extension(cfg.output_model_format)
+        if os.path.isdir(dest) and ext:
+            return os.path.join(dest, f"{cfg.save_filename_prefix}{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}{ext}")
         return dest
 
     def _is_update_step(self, tp: TrainProgress) -> bool:
@@ -189,44 +234,123 @@ class GenericTrainer:
             setup.after_optimizer_step(model, cfg, tp)
         else:
             store.accumulating = True
+        self._has_gradient = not update
+        self.one_step_trained = True
         tp.next_step(cfg.batch_size)
         return loss.detach()
 
+    # ----- the loop ----------------------------------------------------------------------------
+    def _needs_backup(self, tp) -> bool:
+        """GenericTrainer.py:506-509"""
+        cfg = self.config
+        return self.repeating_action_needed("backup", cfg.backup_after, cfg.backup_after_unit, tp, start_at_zero=False)
+
+    def _needs_save(self, tp) -> bool:
+        """GenericTrainer.py:511-516"""
+        cfg = self.config
+        return (self.single_action_elapsed("save_skip_first", cfg.save_skip_first, cfg.save_every_unit, tp)
+                and self.repeating_action_needed("save", cfg.save_every, cfg.save_every_unit, tp, start_at_zero=False))
+
+    def _agree(self, flags: int, step: int) -> int:
+        """Ranks must take a backup / save together (both barrier).  STEP / EPOCH timers agree by
+        construction; a wall-clock timer can fire on one rank and not another, so with one in use
+        rank 0's decision is published through the process group's store (host TCP, no device
+        sync) and every rank acts on it."""
+        if self.world == 1 or not self._wallclock_timers:
+            return flags
+        store = torch.distributed.distributed_c10d._get_default_store()
+        key = f"otamd/actions/{step}"
+        if self.rank == 0:
+            store.set(key, str(flags))
+            return flags
+        return int(store.get(key).decode())
+
     def train(self, log_every: int = 10, max_steps: int | None = None):
+        """GenericTrainer.py:600-749 around train_step(): backup_after / save_every timers raise the
+        backup / save commands before a step; the commands run at the next optimizer-update boundary
+        (no accumulated gradient pending); stop is checked after every step and epoch."""
         cfg = self.config
         tp = self.model.train_progress
         if self.data_loader is None:
             raise RuntimeError("no data: set cache_dir to a latent cache or configure concepts")
+        self._wallclock_timers = any(TimedActionMixin._unit(u) in ("SECOND", "MINUTE", "HOUR")
+                                     for u in (cfg.backup_after_unit, cfg.save_every_unit))
         steps = 0
-        for _epoch in range(tp.epoch, cfg.epochs):
-            self.data_loader.get_data_set().start_next_epoch()
-            for batch in self.data_loader.get_data_loader():
-                loss = self.train_step(batch)
-                self.loss_history.append(loss)
-                steps += 1
-                if steps == 1:
-                    # long-lived objects (model, plans, workspaces) out of the collector's generations; cyclic GC
-                    # then runs only at the log points below, not as a pause inside a step's kernel issue
-                    gc.collect()
-                    gc.freeze()
-                    gc.disable()
-                if log_every and steps % log_every == 0:
-                    gc.collect()
-                    vals = torch.stack(self.loss_history[-log_every:]).float()
-                    if self.world > 1:
-                        torch.distributed.all_reduce(vals)
-                        vals /= self.world
-                    if self.rank == 0:
-                        print(f"step {tp.global_step}: loss {vals.mean().item():.5f}", flush=True)
-                if self.commands is not None and getattr(self.commands, "get_stop_command", lambda: False)():
-                    gc.enable()
+        frozen = False
+        try:
+            for _epoch in range(tp.epoch, cfg.epochs):
+                self.data_loader.get_data_set().start_next_epoch()
+                for batch in self.data_loader.get_data_loader():
+                    if self._needs_backup(tp):
+                        self.commands.backup()
+                    if self._needs_save(tp):
+                        self.commands.save()
+                    if not self._has_gradient:
+                        flags = (int(self.commands.get_and_reset_backup_command())
+                                 | int(self.commands.get_and_reset_save_command()) << 1)
+                        flags = self._agree(flags, tp.global_step)
+                        if flags & 1:
+                            self.backup(tp)
+                        if flags & 2:
+                            self.save(tp)
+                    loss = self.train_step(batch)
+                    self.loss_history.append(loss)
+                    steps += 1
+                    if steps == 1:
+                        # long-lived objects (model, plans, workspaces) out of the collector's generations; cyclic
+                        # GC then runs only at the log points below, not as a pause inside a step's kernel issue
+                        gc.collect()
+                        gc.freeze()
+                        gc.disable()
+                        frozen = True
+                    if log_every and steps % log_every == 0:
+                        gc.collect()
+                        self._report_losses(log_every)
+                    if self.commands.get_stop_command():
+                        return
+                    if max_steps is not None and steps >= max_steps:
+                        return
+                tp.next_epoch()
+                if self.commands.get_stop_command():
                     return
-                if max_steps is not None and steps >= max_steps:
-                    gc.enable()
-                    return
-            tp.next_epoch()
-        gc.enable()
+        finally:
+            if frozen:
+                gc.unfreeze()
+            gc.enable()
+
+    def _report_losses(self, n: int):
+        vals = torch.stack(self.loss_history[-n:]).float()
+        if self.world > 1:
+            torch.distributed.all_reduce(vals)
+            vals /= self.world
+        if self.rank == 0:
+            print(f"step {self.model.train_progress.global_step}: loss {vals.mean().item():.5f} "
+                  f"lr {self.lr_scheduler.get_last_lr()[0]:.3e}", flush=True)
+        del self.loss_history[:-n]
 
     def end(self):
+        """GenericTrainer.py:766-806: after at least one trained step, a backup first when
+        backup_before_save is set, then the final model to output_model_destination in
+        output_model_format / output_dtype (rank 0 writes)."""
         if torch.cuda.is_available():
             torch.cuda.synchronize()
+        if not self.one_step_trained:
+            return None
+        cfg = self.config
+        if cfg.backup_before_save:
+            self.backup(self.model.train_progress)
+        path = self.final_model_path()
+        if self.rank == 0:
+            print("Saving " + path)
+        return self._write_model(path, cfg.output_model_format)
+
+
+def _file_extension(fmt: str) -> str:
+    """ModelFormat.file_extension (modules/util/enum/ModelFormat.py)"""
+    return {"CKPT": ".ckpt", "SAFETENSORS": ".safetensors", "LEGACY_SAFETENSORS": ".safetensors"}.get(str(fmt), "")
+
+
+def _torch_dtype(name: str):
+    """DataType.torch_dtype (modules/util/enum/DataType.py:19-36)"""
+    return {"FLOAT_32": torch.float32, "TFLOAT_32": torch.float32, "BFLOAT_16": torch.bfloat16,
+            "FLOAT_16": torch.float16}.get(str(name))

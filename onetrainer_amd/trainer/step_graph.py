@@ -49,6 +49,10 @@ class StepGraphs:
         if os.environ.get("OTAMD_STEP_GRAPH", "0") != "1":
             return False
         setup, cfg = trainer.model_setup, trainer.config
+        # an overlapped optimizer update orders the next forward through host-side waits (PRef.w ->
+        # wait_params) that a replayed graph would skip: the two opt-ins are exclusive
+        if getattr(trainer.model.optimizer, "overlap", False):
+            return False
         return (trainer.device.type == "cuda" and trainer.world == 1 and trainer.reducer is None
                 and cfg.gradient_accumulation_steps == 1 and hasattr(setup, "graphable")
                 and hasattr(setup, "step_inputs") and setup.graphable(cfg))

@@ -95,12 +95,21 @@ class TrainConfig:
     base_model_name: str = ""
     vae_model_name: str = ""
     lora_model_name: str = ""
-    output_model_destination: str = ""
+    output_model_destination: str = "models/model.safetensors"   # TrainConfig.py:783-785
     output_model_format: str = "SAFETENSORS"
+    output_dtype: str = "FLOAT_32"
     workspace_dir: str = "workspace/run"
     continue_last_backup: bool = False
+    # periodic backups / saves (TrainConfig.py:981-989)
+    backup_after: float = 30
+    backup_after_unit: str = "MINUTE"
     rolling_backup: bool = False
     rolling_backup_count: int = 3
+    backup_before_save: bool = True
+    save_every: int = 0
+    save_every_unit: str = "NEVER"
+    save_skip_first: int = 0
+    save_filename_prefix: str = ""
     # concepts (TrainConfig.py:793-794): inline list of ConceptConfig dicts, else the concept file
     concepts: list | None = None
     concept_file_name: str = "training_concepts/concepts.json"

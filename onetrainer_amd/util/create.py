@@ -29,6 +29,8 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
                                        trainable=config.training_method != "LORA")
         return FluxModel(tr, model_type=mt)
     if unet_config is None:
+        unet_config = _unet_config_on_disk(config)
+    if unet_config is None:
         if mt.startswith("STABLE_DIFFUSION_XL"):
             unet_config = U.sdxl_config()
         elif is_sd15(mt):
@@ -38,6 +40,25 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
     unet = U.UNet2DConditionModel(unet_config, device, seed=seed, trainable=config.training_method != "LORA")
     ns = NoiseScheduler(device, prediction_type=prediction_type)
     return StableDiffusionXLModel(unet, ns, SCALING.get(mt, 0.13025), model_type=mt)
+
+
+def _unet_config_on_disk(config):
+    """the architecture a diffusers-layout model directory declares (`unet/config.json`, as
+    diffusers' from_pretrained reads it): the backup continued from, else base_model_name.
+    Single-file checkpoints carry no config and keep the model type's architecture."""
+    import json
+    import os
+    names = []
+    if getattr(config, "continue_last_backup", False) and config.training_method != "LORA":
+        last = config.get_last_backup_path() if hasattr(config, "get_last_backup_path") else None
+        names.append(last)
+    names.append(getattr(config, "base_model_name", None))
+    for name in names:
+        path = os.path.join(name, "unet", "config.json") if name else None
+        if path and os.path.isfile(path):
+            with open(path) as f:
+                return U.unet_config_from_diffusers(json.load(f))
+    return None
 
 
 def is_sd15(model_type: str) -> bool:

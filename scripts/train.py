@@ -29,19 +29,6 @@ class TrainCallbacks:
         print(status, flush=True)
 
 
-class TrainCommands:
-    """modules/util/commands/TrainCommands.py surface: stop flag polled once per step."""
-
-    def __init__(self):
-        self._stop = False
-
-    def stop(self):
-        self._stop = True
-
-    def get_stop_command(self) -> bool:
-        return self._stop
-
-
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description="One Trainer (MI355X build) training script")
     ap.add_argument("--config-path", type=str, required=True, dest="config_path")
@@ -55,6 +42,7 @@ def parse_args(argv=None):
 def main(argv=None):
     args = parse_args(argv)
     from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util.TrainCommands import TrainCommands
     from onetrainer_amd.util.config.TrainConfig import TrainConfig
 
     callbacks = TrainCallbacks()
@@ -76,8 +64,9 @@ def main(argv=None):
         trainer.train(max_steps=args.max_steps)
     except KeyboardInterrupt:
         canceled = True
-    if not canceled or train_config.extra.get("backup_before_save", True):
+    if not canceled or train_config.backup_before_save:   # scripts/train.py:36-43
         trainer.end()
+    return trainer
 
 
 if __name__ == "__main__":

@@ -1,7 +1,8 @@
 """scripts/train.py (the reference's scripts/train.py:15-43 on this build): a reference-format
 JSON config -> GenericTrainer(config, callbacks, commands).start() / train() / end(), reading a
 latent cache written by LatentCacheWriter (SD 1.5 full UNet, random init, 128^2 images in two
-aspect buckets)."""
+aspect buckets), then the loop's external behaviour: periodic backups (backup_after 1 STEP, rolling 2)
+and end()'s backup-before-save + final model, reloaded through the model loader."""
 import json
 
 import pytest
@@ -16,11 +17,22 @@ def test_train_script_runs_reference_config(dev, tmp_path):
 
     from onetrainer_amd.dataLoader.aspect_bucketing import AspectBucketing
     from onetrainer_amd.dataLoader.latent_cache import LatentCacheWriter
+    from onetrainer_amd.modelLoader.StableDiffusionModelLoader import StableDiffusionXLModelLoader
+    from onetrainer_amd.modelSaver import StableDiffusionXLModelSaver
+    from onetrainer_amd.module import unet as U
     from onetrainer_amd.module import vae as V
+    from onetrainer_amd.util import create
+    from onetrainer_amd.util.ModelNames import ModelNames
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
     torch.manual_seed(0)
+    # the base model: a tiny SD 1.5-shaped UNet in diffusers layout (its unet/config.json sets the architecture)
+    base_cfg = TrainConfig.default_values()
+    base_cfg.model_type = "STABLE_DIFFUSION_15"
+    base = create.create_model(base_cfg, dev, seed=5, unet_config=U.tiny_sd15_config())
+    StableDiffusionXLModelSaver().save(base, None, "DIFFUSERS", str(tmp_path / "base"))
     enc = V.AutoencoderKLEncoder(V.tiny_vae_config(), dev, seed=1)
     shapes = [(128, 128), (128, 128), (128, 192), (128, 192)]   # SD 1.5 latents: multiples of 8
-    samples = [{"image": torch.rand(3, h, w), "text": {"text_encoder_hidden_state": torch.randn(77, 768).bfloat16()}}
+    samples = [{"image": torch.rand(3, h, w), "text": {"text_encoder_hidden_state": torch.randn(77, 96).bfloat16()}}
                for h, w in shapes]
     cache = tmp_path / "cache"
     LatentCacheWriter(lambda im: enc.encode(im), str(cache), AspectBucketing(128, 64), dev, encode_batch=2).write(samples)
@@ -28,10 +40,32 @@ def test_train_script_runs_reference_config(dev, tmp_path):
            "cache_dir": str(cache), "batch_size": 2, "epochs": 1, "learning_rate": 1e-5,
            "learning_rate_warmup_steps": 0, "workspace_dir": str(tmp_path / "ws"), "train_dtype": "BFLOAT_16",
            "optimizer": {"optimizer": "ADAMW", "stochastic_rounding": True},
-           "unet": {"train": True}, "text_encoder": {"train": False}}
+           "unet": {"train": True}, "text_encoder": {"train": False}, "base_model_name": str(tmp_path / "base"),
+           "output_model_destination": str(tmp_path / "out" / "model.safetensors"), "output_model_format": "SAFETENSORS",
+           "output_dtype": "FLOAT_32", "backup_after": 1, "backup_after_unit": "STEP", "rolling_backup": True,
+           "rolling_backup_count": 2}
     path = tmp_path / "config.json"
     path.write_text(json.dumps(cfg))
     spec = importlib.util.spec_from_file_location("train_script", Path(__file__).parents[1] / "scripts" / "train.py")
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    mod.main(["--config-path", str(path)])
+    tr = mod.main(["--config-path", str(path)])
+    tp = tr.model.train_progress
+    assert tp.global_step == 2 and tr.model.unet.cfg == U.tiny_sd15_config()
+    # backups before steps 0 and 1 and before the final save; the rolling window keeps the newest 2
+    backups = sorted((tmp_path / "ws" / "backup").iterdir())
+    assert len(backups) == 2, backups
+    steps = sorted(json.loads((b / "meta.json").read_text())["train_progress"]["global_step"] for b in backups)
+    assert steps == [1, 2], steps
+    # the final model reloads through the model loader with the trained weights (bf16 -> fp32 -> bf16 is exact)
+    out = tmp_path / "out" / "model.safetensors"
+    assert out.is_file()
+    fresh = create.create_model(base_cfg, dev, seed=11, unet_config=U.tiny_sd15_config())
+    StableDiffusionXLModelLoader().load(fresh, ModelNames(base_model=str(out)))
+    trained, loaded = tr.model.unet.state_dict(), fresh.unet.state_dict()
+    assert trained.keys() == loaded.keys()
+    for k in trained:
+        assert torch.equal(trained[k], loaded[k]), k
+    base_sd = base.unet.state_dict()
+    moved = sum(not torch.equal(trained[k], base_sd[k]) for k in trained)
+    assert moved > 0.5 * len(trained)      # the saved weights are the trained ones, not the base

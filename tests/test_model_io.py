@@ -177,3 +177,33 @@ def test_flux_diffusers_roundtrip(tmp_path):
     assert cfg["num_layers"] == 2 and cfg["num_single_layers"] == 2
     FluxModelLoader().load(dst, ModelNames(base_model=str(tmp_path / "flux")))
     assert _same(src.transformer, dst.transformer)
+
+
+@pytest.mark.parametrize("name", ["sdxl_config", "sd15_config", "tiny_sdxl_config", "tiny_sd15_config"])
+def test_unet_config_roundtrips_through_diffusers_json(name):
+    """the architecture a saved diffusers directory declares rebuilds the same UNetConfig (the
+    model factory builds the network from `unet/config.json` like from_pretrained)."""
+    from onetrainer_amd.modelSaver import unet_diffusers_config
+    from onetrainer_amd.module import unet as U
+    cfg = getattr(U, name)()
+    back = U.unet_config_from_diffusers(json.loads(json.dumps(unet_diffusers_config(cfg))))
+    assert U.unet_specs(back) == U.unet_specs(cfg)
+    assert back.heads(cfg.block_out_channels[-1]) == cfg.heads(cfg.block_out_channels[-1])
+
+
+def test_unet_config_from_stock_diffusers_json():
+    """diffusers' own SDXL / SD 1.5 config.json shapes (head COUNTS in attention_head_dim, int
+    transformer_layers_per_block for SD 1.5) give the pinned architectures."""
+    from onetrainer_amd.module import unet as U
+    sdxl = {"block_out_channels": [320, 640, 1280], "attention_head_dim": [5, 10, 20],
+            "down_block_types": ["DownBlock2D", "CrossAttnDownBlock2D", "CrossAttnDownBlock2D"],
+            "up_block_types": ["CrossAttnUpBlock2D", "CrossAttnUpBlock2D", "UpBlock2D"],
+            "transformer_layers_per_block": [1, 2, 10], "cross_attention_dim": 2048, "use_linear_projection": True,
+            "addition_embed_type": "text_time", "addition_time_embed_dim": 256,
+            "projection_class_embeddings_input_dim": 2816, "layers_per_block": 2}
+    sd15 = {"block_out_channels": [320, 640, 1280, 1280], "attention_head_dim": 8,
+            "down_block_types": ["CrossAttnDownBlock2D"] * 3 + ["DownBlock2D"],
+            "up_block_types": ["UpBlock2D"] + ["CrossAttnUpBlock2D"] * 3, "cross_attention_dim": 768,
+            "layers_per_block": 2}
+    assert U.unet_specs(U.unet_config_from_diffusers(sdxl)) == U.unet_specs(U.sdxl_config())
+    assert U.unet_specs(U.unet_config_from_diffusers(sd15)) == U.unet_specs(U.sd15_config())

@@ -44,7 +44,16 @@ def test_train_step_matches_oracle(dev, ptype):
     ehs = torch.cat([batch["text_encoder_1_hidden_state"], batch["text_encoder_2_hidden_state"]], -1).float().cpu()
     te = batch["text_encoder_2_pooled_state"].float().cpu()
     tid = torch.tensor([[res, res, 0, 0, res, res]] * 2, dtype=torch.float32)
-    ours, ref = [], []
+    ours, ref, cos = [], [], []
+    cap = {}
+    orig = tr.model_setup.predict
+
+    def capture(*a, **k):
+        out = orig(*a, **k)
+        cap["pred"] = out["predicted"].detach().float().cpu()
+        return out
+
+    tr.model_setup.predict = capture
     for step in range(3):
         gs = model.train_progress.global_step
         noise = K.noise((2, res // 8, res // 8, 4), seed=gs, dtype=torch.float32, device=dev)
@@ -57,13 +66,22 @@ def test_train_step_matches_oracle(dev, ptype):
         xt = OD.add_noise_ddpm(x0, eps, tc, betas)
         pred = om(xt.bfloat16().float(), tc, ehs, te, tid)
         target = eps if ptype == "epsilon" else OD.get_velocity(x0, eps, tc, betas)
-        loss = OD.diffusion_losses(pred, target, torch.ones(2)).mean()
+        per_sample = OD.diffusion_losses(pred, target, torch.ones(2))
+        loss = per_sample.mean()
         loss.backward()
         opt.step()                                   # bf16 clip_grad_norm_ + patched AdamW (pinned oracle)
         ref.append(loss.item())
-    print("losses hip", ours, "oracle", ref)
+        # element by element, not only the scalar: the bf16 network's prediction against the fp32 oracle's,
+        # and each sample's loss (a batch mean can hide per-sample differences that cancel)
+        hp = cap["pred"]
+        cos.append(torch.nn.functional.cosine_similarity(hp.flatten(), pred.detach().flatten(), dim=0).item())
+        hs = OD.diffusion_losses(hp, target, torch.ones(2))
+        assert torch.allclose(hs, per_sample.detach(), rtol=1e-3, atol=0), (step, hs, per_sample)
+        assert 0 < (hp - pred.detach()).abs().max() < 0.05, step      # bf16-sized, and not the oracle's own values
+    print("losses hip", ours, "oracle", ref, "prediction cosine", cos)
     for a, b in zip(ours, ref):                      # north star: loss within rtol 1e-3 of the reference
         assert abs(a - b) <= 1e-3 * abs(b), (ours, ref)
+    assert min(cos) > 0.999, cos
 
 
 def test_sd15_train_step_matches_oracle(dev):

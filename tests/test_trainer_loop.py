@@ -1,0 +1,182 @@
+"""The train loop around the step (CPU): action timers pinned to the reference's own
+TimedActionMixin (tests/golden/timed_actions.json), backup / save commands executed at
+optimizer-update boundaries (GenericTrainer.py:653-668), stop, end() (GenericTrainer.py:766-806).
+train_step / backup / save / the model writer are replaced by recorders: no GPU, no model."""
+import json
+from pathlib import Path
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+from onetrainer_amd.trainer import GenericTrainer as GT
+from onetrainer_amd.util.config.TrainConfig import TrainConfig
+from onetrainer_amd.util.TimedActionMixin import TimedActionMixin
+from onetrainer_amd.util.TrainCommands import TrainCommands
+from onetrainer_amd.util.TrainProgress import TrainProgress
+
+FIX = json.loads((Path(__file__).parent / "golden" / "timed_actions.json").read_text())
+
+
+@pytest.mark.parametrize("case", FIX["cases"], ids=lambda c: f"{c['unit']}-{c['interval']}-{c['skip']}")
+def test_timers_match_reference(case):
+    m = TimedActionMixin()
+    got = {"repeat0": [], "repeat1": [], "single": [], "save": []}
+    for e in range(FIX["epochs"]):
+        for s in range(FIX["steps"]):
+            tp = TrainProgress(epoch=e, epoch_step=s, global_step=e * FIX["steps"] + s)
+            u, n, k = case["unit"], case["interval"], case["skip"]
+            got["repeat0"].append(m.repeating_action_needed("a", n, u, tp, start_at_zero=False))
+            got["repeat1"].append(m.repeating_action_needed("b", n, u, tp, start_at_zero=True))
+            got["single"].append(m.single_action_elapsed("c", k, u, tp))
+            got["save"].append(m.single_action_elapsed("d", k, u, tp)
+                               and m.repeating_action_needed("e", n, u, tp, start_at_zero=False))
+    for key in got:
+        assert got[key] == case[key], key
+
+
+def test_wallclock_timer_starts_at_first_query(monkeypatch):
+    import onetrainer_amd.util.TimedActionMixin as TM
+    now = [1000.0]
+    monkeypatch.setattr(TM.time, "time", lambda: now[0])
+    m = TimedActionMixin()
+    tp = TrainProgress()
+    assert not m.repeating_action_needed("b", 1, "MINUTE", tp, start_at_zero=False)
+    now[0] += 59
+    assert not m.repeating_action_needed("b", 1, "MINUTE", tp, start_at_zero=False)
+    now[0] += 2
+    assert m.repeating_action_needed("b", 1, "MINUTE", tp, start_at_zero=False)
+    assert not m.repeating_action_needed("b", 1, "MINUTE", tp, start_at_zero=False)
+    assert m.repeating_action_needed("z", 1, "MINUTE", tp, start_at_zero=True)   # fires at once
+
+
+def test_config_defaults_match_reference():
+    d = TrainConfig.default_values()
+    for k, v in FIX["defaults"].items():
+        assert getattr(d, k) == v, k
+
+
+class _Loader:
+    def __init__(self, n):
+        self.n = n
+
+    def get_data_set(self):
+        return SimpleNamespace(start_next_epoch=lambda: None, approximate_length=lambda: self.n)
+
+    def get_data_loader(self):
+        return iter(range(self.n))
+
+
+def _trainer(ga=1, epochs=2, steps=6, **cfg_kw):
+    cfg = TrainConfig.default_values()
+    cfg.gradient_accumulation_steps = ga
+    cfg.epochs = epochs
+    for k, v in cfg_kw.items():
+        setattr(cfg, k, v)
+    tp = TrainProgress()
+    tr = GT.GenericTrainer(cfg, model=SimpleNamespace(train_progress=tp), data_loader=_Loader(steps))
+    log = []
+
+    def step(batch):
+        update = tr._is_update_step(tp)
+        log.append(("step", tp.global_step))
+        tr._has_gradient = not update
+        tr.one_step_trained = True
+        tp.next_step(cfg.batch_size)
+        return torch.zeros(())
+
+    tr.train_step = step
+    tr.backup = lambda t=None: log.append(("backup", tp.global_step))
+    tr.save = lambda t=None: log.append(("save", tp.global_step))
+    return tr, log
+
+
+def _actions(log, kind):
+    return [g for k, g in log if k == kind]
+
+
+def test_backup_every_two_steps():
+    tr, log = _trainer(backup_after=2, backup_after_unit="STEP")
+    tr.train(log_every=0)
+    # GenericTrainer.__needs_backup fires when (global_step + 1) % 2 == 0 and runs before that step
+    assert _actions(log, "backup") == [1, 3, 5, 7, 9, 11]
+    assert _actions(log, "save") == []
+
+
+def test_commands_wait_for_the_update_boundary():
+    """with GA=2 a backup raised on a micro-step with a gradient pending runs before the next
+    update-cycle's first micro-step (GenericTrainer.py:653-668 `if not has_gradient`)."""
+    tr, log = _trainer(ga=2, backup_after=2, backup_after_unit="STEP")
+    tr.train(log_every=0)
+    assert _actions(log, "backup") == [2, 4, 6, 8, 10]
+
+
+def test_save_every_epoch_after_skip():
+    tr, log = _trainer(epochs=3, steps=4, save_every=1, save_every_unit="EPOCH", save_skip_first=1)
+    tr.train(log_every=0)
+    # epoch-unit saves fire at the first step of each epoch after the first (start_at_zero=False), and
+    # save_skip_first=1 EPOCH skips none of those (epoch + 1 > 1 from epoch 1 on)
+    assert _actions(log, "save") == [4, 8]
+
+
+def test_external_commands_and_stop():
+    cmds = TrainCommands()
+    tr, log = _trainer(steps=10, backup_after_unit="NEVER")
+    tr.commands = cmds
+    orig = tr.train_step
+
+    def step(batch):
+        g = tr.model.train_progress.global_step
+        if g == 2:
+            cmds.save()
+        if g == 5:
+            cmds.stop()
+        return orig(batch)
+
+    tr.train_step = step
+    tr.train(log_every=0)
+    assert _actions(log, "save") == [3]
+    assert _actions(log, "step")[-1] == 5     # stop is honoured right after the step that raised it
+    assert not cmds.get_and_reset_save_command()
+
+
+def test_gc_restored_after_an_exception():
+    import gc
+    tr, log = _trainer(steps=5)
+    orig = tr.train_step
+
+    def step(batch):
+        if tr.model.train_progress.global_step == 3:
+            raise KeyboardInterrupt
+        return orig(batch)
+
+    tr.train_step = step
+    with pytest.raises(KeyboardInterrupt):
+        tr.train(log_every=0)
+    assert gc.isenabled()
+    assert gc.get_freeze_count() == 0
+
+
+def test_end_backs_up_then_saves(tmp_path):
+    tr, log = _trainer(steps=2, output_model_destination=str(tmp_path), output_model_format="SAFETENSORS",
+                       save_filename_prefix="run-", output_dtype="BFLOAT_16")
+    written = []
+    tr._write_model = lambda path, fmt: written.append((path, fmt, tr.config.output_dtype)) or path
+    assert tr.end() is None and written == []          # nothing trained: nothing saved (GenericTrainer.py:767)
+    tr.train(log_every=0)
+    tr.end()
+    assert _actions(log, "backup") == [4]             # backup_before_save (default True)
+    (path, fmt, dt), = written
+    assert fmt == "SAFETENSORS" and dt == "BFLOAT_16"
+    assert Path(path).parent == tmp_path and Path(path).name.startswith("run-") and path.endswith(".safetensors")
+    assert GT._torch_dtype("BFLOAT_16") is torch.bfloat16 and GT._torch_dtype("FLOAT_32") is torch.float32
+
+
+def test_end_without_backup_to_a_file(tmp_path):
+    dest = str(tmp_path / "out" / "model.safetensors")
+    tr, log = _trainer(steps=1, output_model_destination=dest, backup_before_save=False)
+    written = []
+    tr._write_model = lambda path, fmt: written.append(path) or path
+    tr.train(log_every=0)
+    tr.end()
+    assert written == [dest] and _actions(log, "backup") == []
