@@ -97,10 +97,14 @@ def cpu_baseline(res=512, sd15=False, warmup=1, timed=3):
     return times, threads
 
 
-def gemm_roofline(tr, batch):
+def gemm_roofline(tr, batch, in_step: bool = True):
     """Dominant kernel family (bf16 MFMA GEMM / implicit-GEMM conv: gemm2_kernel<*>, gemm_kernel,
     splitk_reduce): one extra, untimed train step with a HIP event pair around every GEMM launch on
-    the stream it is launched on.  achieved = sum(2 M N K) / sum(launch durations)."""
+    the stream it is launched on.  achieved = sum(2 M N K) / sum(launch durations).
+
+    in_step=True: the step exactly as timed (weight-gradient GEMMs on the side stream, concurrent with the
+    dgrad chain), so the durations are the in-step ones a rocprofv3 kernel trace of the timed steps
+    reports (profiles/r3_kstats_*.csv); in_step=False: side stream off, every GEMM alone on the chip."""
     from onetrainer_amd import kernels as K
     recs = []
     orig = K._gemm
@@ -114,7 +118,8 @@ def gemm_roofline(tr, batch):
 
     from onetrainer_amd.module import streams
     was = streams.enabled()
-    streams.set_enabled(False)   # per-launch durations in isolation (no side-stream overlap)
+    if not in_step:
+        streams.set_enabled(False)
     graphs, tr.graphs = tr.graphs, None   # an eager step: every GEMM launched (and timed) from the host
     K._gemm = timed
     try:
@@ -287,12 +292,14 @@ def main():
     if not math.isfinite(loss_val):
         raise RuntimeError(f"non-finite loss {loss_val}")
 
-    g_flops, g_ms, g_n = gemm_roofline(tr, batch)
+    g_flops, g_ms, g_n = gemm_roofline(tr, batch, in_step=True)
+    i_flops, i_ms, _ = gemm_roofline(tr, batch, in_step=False)
     vae = None
     if not args.no_vae:   # latent caching, reported beside the step, not part of `value`
         from tools.bench_vae import run as vae_run
         vae = vae_run(args.res, args.batch, iters=5, warmup=1, device=str(dev))
     g_achieved = g_flops / (g_ms * 1e-3) / 1e12
+    i_achieved = i_flops / (i_ms * 1e-3) / 1e12
     pmc = pmc_traffic()
 
     imgs = args.batch * world * args.steps
@@ -358,8 +365,12 @@ def main():
                                      "Infinity-Cache hits included), from profiles/pmc_traffic_sdxl1024_b4.json",
                      "algorithmic_gb": round(gemm_roofline.algo_bytes / 1e9, 2),
                      "kernel": "bf16 MFMA GEMM / implicit-GEMM conv (gemm2_kernel<*>, gemm_kernel, splitk_reduce_kernel)",
-                     "basis": f"sum(2*M*N*K) over the {g_n} GEMM/conv launches of one step / sum of their HIP-event "
-                              f"durations ({g_ms:.2f} ms of GEMM per step)",
+                     "basis": f"sum(2*M*N*K) over the {g_n} GEMM/conv launches of one step / sum of their in-step "
+                              f"HIP-event durations ({g_ms:.2f} ms of GEMM kernel time per step, summed over the main "
+                              f"and the weight-gradient stream, which run concurrently)",
+                     "isolated_achieved": round(i_achieved, 1), "isolated_frac": round(i_achieved / PEAK_BF16_TFLOPS, 4),
+                     "isolated_basis": f"the same launches with the side stream off, each GEMM alone on the chip "
+                                       f"({i_ms:.2f} ms per step)",
                      "step_achieved": round(achieved, 1), "step_frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "step_basis": basis + " x per-GPU images / step time"},
         "cpu_baseline": None,
@@ -377,13 +388,13 @@ def main():
         torch.cuda.empty_cache()
         try:
             # C1 (SD 1.5 preset, 512^2, b=1): 1 warm-up + 3 timed, p50; then the bench workload's own
-            # network at its resolution, b=1 (SDXL 1024^2: 1 warm-up + 1 timed) -> `value`
+            # network at its resolution, b=1 (SDXL 1024^2: 1 warm-up + 3 timed, p50) -> `value`
             c1, threads = cpu_baseline(512, sd15=True, warmup=1, timed=3)
             c1_p50 = sorted(c1)[len(c1) // 2]
             if sd15 and args.res == 512:
                 big, big_p50 = c1, c1_p50
             else:
-                big, _ = cpu_baseline(args.res, sd15=sd15, warmup=1, timed=1)
+                big, _ = cpu_baseline(args.res, sd15=sd15, warmup=1, timed=3)   # >= 3 timed
                 big_p50 = sorted(big)[len(big) // 2]
             out["cpu_baseline"] = {
                 "value": round(1.0 / big_p50, 5), "unit": "images/s", "cores": threads, "kind": "port",

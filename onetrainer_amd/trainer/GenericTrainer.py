@@ -26,7 +26,7 @@ from ..util.lr_scheduler_util import create_lr_scheduler
 from ..util.TimedActionMixin import TimedActionMixin
 from ..util.TrainCommands import TrainCommands
 from ..util.TrainProgress import TrainProgress
-from .ddp import GradBucketReducer, init_from_env
+from .ddp import GradBucketReducer, abort, init_from_env
 
 
 class GenericTrainer(TimedActionMixin):
@@ -277,6 +277,7 @@ class GenericTrainer(TimedActionMixin):
                                      for u in (cfg.backup_after_unit, cfg.save_every_unit))
         steps = 0
         frozen = False
+        failed = True
         try:
             for _epoch in range(tp.epoch, cfg.epochs):
                 self.data_loader.get_data_set().start_next_epoch()
@@ -306,17 +307,29 @@ class GenericTrainer(TimedActionMixin):
                     if log_every and steps % log_every == 0:
                         gc.collect()
                         self._report_losses(log_every)
-                    if self.commands.get_stop_command():
-                        return
-                    if max_steps is not None and steps >= max_steps:
+                    if self.commands.get_stop_command() or (max_steps is not None and steps >= max_steps):
+                        failed = False
                         return
                 tp.next_epoch()
                 if self.commands.get_stop_command():
+                    failed = False
                     return
+            failed = False
         finally:
+            if failed and self.world > 1:
+                self.abort_distributed()
             if frozen:
                 gc.unfreeze()
             gc.enable()
+
+    def abort_distributed(self):
+        """a rank failed (exception, timed-out collective, KeyboardInterrupt) inside train(): abort the
+        process group so the rank exits instead of leaving peers blocked in a collective; the peers'
+        own collectives time out (ddp.init_from_env) and abort the same way."""
+        print(f"rank {self.rank}: training failed, aborting the process group", flush=True)
+        self.reducer = None
+        self.world = 1
+        abort()
 
     def _report_losses(self, n: int):
         vals = torch.stack(self.loss_history[-n:]).float()

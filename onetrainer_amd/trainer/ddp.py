@@ -118,8 +118,19 @@ class GradBucketReducer:
         self.arm(True)
 
 
-def init_from_env(backend: str | None = None):
-    """torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT)."""
+DEFAULT_TIMEOUT_S = 600
+
+
+def init_from_env(backend: str | None = None, timeout_s: float | None = None):
+    """torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT).
+
+    Failure detection: every collective of the group carries a timeout
+    (OTAMD_DIST_TIMEOUT_S, default 600 s) -- a rank that died or hangs makes its peers' next
+    collective raise instead of blocking forever -- and RCCL runs with asynchronous error handling
+    (TORCH_NCCL_ASYNC_ERROR_HANDLING=1 unless set: the watchdog tears the communicator down on a
+    timed-out or failed collective).  The trainer then aborts the group and the rank exits with the
+    error (GenericTrainer.abort_distributed)."""
+    import datetime
     import os
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -127,7 +138,22 @@ def init_from_env(backend: str | None = None):
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = os.environ.get("OTAMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("OTAMD_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+        if backend == "nccl":
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if torch.cuda.is_available():
             torch.cuda.set_device(local if backend == "nccl" else local % max(1, torch.cuda.device_count()))
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
     return rank, world, local
+
+
+def abort():
+    """tear the process group down after a failure so this rank can exit (no further collective is
+    attempted; a peer blocked in one times out on its own)."""
+    if dist.is_available() and dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:   # a broken communicator may refuse a clean shutdown; exiting is what matters
+            pass

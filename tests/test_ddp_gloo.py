@@ -126,3 +126,54 @@ def test_bucket_partition_is_contiguous_and_complete():
         if prev_begin is not None:
             assert e <= prev_begin + 8
         prev_begin = b
+
+
+def _worker_dead_peer(rank, world, port, q):
+    """rank 1 dies before the collective; rank 0's all-reduce must time out (ddp.init_from_env's
+    group timeout) and the trainer's abort path must let it exit, not block forever."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), OTAMD_DIST_BACKEND="gloo")
+    import time
+    from types import SimpleNamespace
+
+    from onetrainer_amd.trainer import ddp
+    from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+    from onetrainer_amd.util.TrainProgress import TrainProgress
+    ddp.init_from_env(timeout_s=5)
+    if rank == 1:
+        os._exit(0)          # dies without a word
+    cfg = TrainConfig.default_values()
+    cfg.backup_after_unit = "NEVER"
+    tp = TrainProgress()
+    loader = SimpleNamespace(get_data_set=lambda: SimpleNamespace(start_next_epoch=lambda: None),
+                             get_data_loader=lambda: iter(range(3)))
+    tr = GenericTrainer(cfg, model=SimpleNamespace(train_progress=tp), data_loader=loader)
+    tr.rank, tr.world = rank, world
+
+    def step(batch):          # the gradient all-reduce of a DP step
+        dist.all_reduce(torch.ones(4))
+        tp.next_step(1)
+        return torch.zeros(())
+
+    tr.train_step = step
+    t0 = time.time()
+    try:
+        tr.train(log_every=0)
+        q.put((rank, "no error"))
+    except Exception as e:
+        q.put((rank, f"raised after {time.time() - t0:.0f}s, group initialized: {dist.is_initialized()}"))
+
+
+def test_dead_peer_times_out_and_aborts():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_dead_peer, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    rank, msg = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert rank == 0 and msg.startswith("raised") and msg.endswith("group initialized: False"), msg
+    assert all(p.exitcode is not None for p in procs)

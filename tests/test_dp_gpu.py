@@ -1,4 +1,5 @@
-"""Data-parallel equivalence: two ranks at b=1 each == one rank at b=2.
+"""Data-parallel equivalence: two ranks at b=1 each == one rank at b=2, and four
+ranks at b=1 with gradient accumulation 2 == one rank at b=4 with GA 2.
 
 The ranks are fresh child processes on the one GPU of the test box (torch.distributed 'gloo'
 with HIP tensors: RCCL cannot put two ranks on one device), each running
@@ -36,7 +37,7 @@ def _port():
     return p
 
 
-def _run(tmp, world, fp32=False):
+def _run(tmp, world, fp32=False, global_batch=2, ga=1):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -47,8 +48,9 @@ def _run(tmp, world, fp32=False):
         if world > 1:
             e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                      MASTER_PORT=str(port), OTAMD_DIST_BACKEND="gloo")
-        out = tmp / f"w{world}_{int(fp32)}_r{r}.pt"
-        cmd = [sys.executable, str(WORKER), "--global-batch", "2", "--out", str(out)] + (["--fp32-reduce"] if fp32 else [])
+        out = tmp / f"w{world}_{int(fp32)}_{global_batch}_{ga}_r{r}.pt"
+        cmd = [sys.executable, str(WORKER), "--global-batch", str(global_batch), "--out", str(out), "--ga", str(ga),
+               "--steps", str(ga)] + (["--fp32-reduce"] if fp32 else [])
         procs.append(subprocess.Popen(cmd, env=e))
         outs.append(out)
     for p in procs:
@@ -56,14 +58,13 @@ def _run(tmp, world, fp32=False):
     return [torch.load(o, weights_only=True) for o in outs]
 
 
-@pytest.mark.parametrize("fp32", [False, True])
-def test_dp2_equals_single_rank_global_batch(tmp_path, fp32):
-    ref = _run(tmp_path, 1)[0]
-    r0, r1 = _run(tmp_path, 2, fp32)
-    loss_dp = (r0["loss"] + r1["loss"]) / 2
+def _compare(ranks, ref, fp32, label):
+    r0 = ranks[0]
+    loss_dp = sum(r["loss"] for r in ranks) / len(ranks)
     torch.testing.assert_close(loss_dp, ref["loss"], rtol=1e-5, atol=0)
-    torch.testing.assert_close(r0["norm"], ref["norm"], rtol=2e-3, atol=0)
-    assert torch.equal(r0["grad"], r1["grad"]) and torch.equal(r0["param"], r1["param"])   # replicas identical
+    torch.testing.assert_close(r0["norm"][-1], ref["norm"][-1], rtol=2e-3, atol=0)
+    for r in ranks[1:]:    # replicas identical
+        assert torch.equal(r0["grad"], r["grad"]) and torch.equal(r0["param"], r["param"])
     g, gr = r0["grad"], ref["grad"]
     cos = torch.nn.functional.cosine_similarity(g, gr, dim=0).item()
     rel = ((g - gr).norm() / gr.norm()).item()
@@ -72,7 +73,25 @@ def test_dp2_equals_single_rank_global_batch(tmp_path, fp32):
     ulp = torch.exp2(torch.floor(torch.log2(pr.abs().clamp_min(1e-30))) - 7)      # bf16 spacing at |p|
     excess = ((pa - pr).abs() - (2 * 1e-4 + ulp)).max().item()
     dmax = (pa - pr).abs().max().item()
-    print(f"dp2 vs dp1 ({'fp32' if fp32 else 'bf16'} reduce): grad cos {cos:.7f} rel-L2 {rel:.3e} "
+    print(f"{label} ({'fp32' if fp32 else 'bf16'} reduce): grad cos {cos:.7f} rel-L2 {rel:.3e} "
           f"params differing {diff:.2e} (max {dmax:.2e}) loss {loss_dp.tolist()} vs {ref['loss'].tolist()}")
     assert cos >= 0.9999 and rel <= 1e-2
     assert diff <= 1e-2 and excess <= 0
+    return rel
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_dp2_equals_single_rank_global_batch(tmp_path, fp32):
+    ref = _run(tmp_path, 1)[0]
+    _compare(_run(tmp_path, 2, fp32), ref, fp32, "dp2 vs dp1")
+
+
+def test_dp4_ga2_bf16_vs_fp32_reduce(tmp_path):
+    """four ranks (b=1 each, gradient accumulation 2: the reducer armed on the update micro-step only,
+    over the accumulated sum) against one rank at global batch 4 with GA 2; the bf16 in-place bucket
+    reduction and the fp32 staging (dp_reduce_fp32) side by side at 4 partials -- the data behind the
+    dp_reduce_fp32 default."""
+    ref = _run(tmp_path, 1, global_batch=4, ga=2)[0]
+    rel_bf16 = _compare(_run(tmp_path, 4, False, global_batch=4, ga=2), ref, False, "dp4 ga2 vs dp1 ga2")
+    rel_fp32 = _compare(_run(tmp_path, 4, True, global_batch=4, ga=2), ref, True, "dp4 ga2 vs dp1 ga2")
+    print(f"dp4 reduction error vs world 1: bf16 {rel_bf16:.3e}, fp32 staging {rel_fp32:.3e}")

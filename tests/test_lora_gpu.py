@@ -135,3 +135,63 @@ def test_lora_train_steps(dev):
     s = model.unet_lora.store.slots[ups[0]]
     assert torch.count_nonzero(model.unet_lora.store.data[s.offset:s.offset + s.numel]) > 0
     assert not torch.equal(model.unet_lora.store.data, lora0)
+
+
+def test_sdxl_lora_trajectory_matches_oracle(dev):
+    """C4's path at test size: 3 SDXL LoRA train steps (frozen bf16 base, fp32 r8 adapters on every
+    Linear / Conv2d, fp32 AdamW) against the oracle UNet with the reference LoRA hooks
+    (LoRAModule.py:283-323) and the pinned fp32 AdamW restatement (adamw_extensions.py:17-150), on the
+    same weights, noise and timesteps: every step's loss at rtol 1e-3 (the adapters' up weights start
+    at zero, so steps 2 and 3 carry the trained adapters)."""
+    from _oracle_opt import OracleF32AdamW
+    from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_sdxl_batch
+    from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util import create
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+    from oracle import diffusion as OD
+
+    ucfg = U.tiny_sdxl_config()
+    cfg = TrainConfig.default_values()
+    cfg.training_method = "LORA"
+    cfg.batch_size = 2
+    cfg.learning_rate = 3e-4
+    cfg.learning_rate_warmup_steps = 0
+    cfg.lora_rank, cfg.lora_alpha = 8, 8.0
+    cfg.optimizer.stochastic_rounding = False
+    model = create.create_model(cfg, dev, seed=3, unet_config=ucfg)
+    tr = GenericTrainer(cfg, model=model)
+    tr.start()
+    om = OU.UNet2DConditionModel(OU.UNetConfig(**{k: getattr(ucfg, k) for k in OU.UNetConfig.__dataclass_fields__}))
+    om.load_state_dict({k: v.float().cpu() for k, v in model.unet.state_dict().items()})
+    om.requires_grad_(False)
+    ol = OracleLoRA(om, 8, 8.0)
+    ol.load_state_dict({k: v.float().cpu() for k, v in model.unet_lora.state_dict().items() if not k.endswith(".alpha")})
+    assert len(ol.params) == len([k for k in model.unet_lora.state_dict() if not k.endswith(".alpha")])
+    opt = OracleF32AdamW(ol.parameters(), lr=3e-4, weight_decay=1e-2)
+    res = 128
+    batch = synthetic_sdxl_batch(2, res, res, dev, seed=1, te1_dim=48, te2_dim=48, pooled_dim=64)
+    betas = OD.scaled_linear_betas()
+    lat = batch["latent_image"].cpu().float()
+    ehs = torch.cat([batch["text_encoder_1_hidden_state"], batch["text_encoder_2_hidden_state"]], -1).float().cpu()
+    te = batch["text_encoder_2_pooled_state"].float().cpu()
+    tid = torch.tensor([[res, res, 0, 0, res, res]] * 2, dtype=torch.float32)
+    base0 = model.unet.store.data.clone()
+    ours, ref = [], []
+    for step in range(3):
+        gs = model.train_progress.global_step
+        noise = K.noise((2, res // 8, res // 8, 4), seed=gs, dtype=torch.float32, device=dev)
+        t = K.timesteps(2, seed=gs, device=dev)
+        ours.append(tr.train_step(batch).item())
+        eps = noise.cpu().permute(0, 3, 1, 2)
+        tc = t.cpu().long()
+        xt = OD.add_noise_ddpm(lat * 0.13025, eps, tc, betas)
+        pred = om(xt.bfloat16().float(), tc, ehs, te, tid)
+        loss = OD.diffusion_losses(pred, eps, torch.ones(2)).mean()
+        loss.backward()
+        opt.step()
+        ref.append(loss.item())
+    print("sdxl lora losses hip", ours, "oracle", ref)
+    for a, b in zip(ours, ref):
+        assert abs(a - b) <= 1e-3 * abs(b), (ours, ref)
+    assert ref[1] != ref[0] and ours[2] != ours[1]
+    assert torch.equal(model.unet.store.data, base0)

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--fp32-reduce", action="store_true")
     ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--ga", type=int, default=1, help="gradient accumulation steps (run --steps = ga for one update)")
     args = ap.parse_args()
     import torch
 
@@ -45,6 +46,7 @@ def main():
     cfg.optimizer.stochastic_rounding = False
     cfg.dp_reduce_fp32 = args.fp32_reduce
     cfg.dp_bucket_mb = 1            # many buckets: exercises the progressive launch
+    cfg.gradient_accumulation_steps = args.ga
     model = create.create_model(cfg, dev, seed=3, unet_config=U.tiny_sdxl_config())
     tr = GenericTrainer(cfg, model=model)
     tr.start()

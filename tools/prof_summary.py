@@ -27,11 +27,11 @@ def main() -> None:
         steps = sum(r[1] for r in rows if a.steps_kernel in r[0]) or 1
     else:
         # only whole steps between optimizer launches, skipping the first window (model init, first-shape
-        # planning, warm-up) and the last one (bench.py's extra roofline step runs after the timed steps)
+        # planning, warm-up) and the last two (bench.py's two extra roofline steps run after the timed steps)
         ev = c.execute("select name, start, end from kernels order by start").fetchall()
         marks = [s for n, s, e in ev if a.steps_kernel in n]
-        lo, hi = marks[1], marks[-2]
-        steps = max(1, len(marks) - 3)
+        lo, hi = marks[1], marks[-3]
+        steps = max(1, len(marks) - 4)
         agg = {}
         for n, s, e in ev:
             if lo < s <= hi:

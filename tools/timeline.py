@@ -1,5 +1,5 @@
-"""Per-step timeline statistics from a rocprofv3 kernel-trace DB: for the last train step (between
-the last two fused-AdamW launches) the busy time of each stream, the union of busy time (GPU
+"""Per-step timeline statistics from a rocprofv3 kernel-trace DB: for the last timed train step
+(between fused-AdamW launches) the busy time of each stream, the union of busy time (GPU
 occupied by >= 1 kernel), the idle gaps, and the per-stream top kernels.
 
 usage: python tools/timeline.py gpurun_out/prof/run_results.db [--marker adamw_bf16_kernel]
@@ -7,6 +7,19 @@ usage: python tools/timeline.py gpurun_out/prof/run_results.db [--marker adamw_b
 import argparse
 import collections
 import sqlite3
+
+
+CATS = [("gemm2_kernel", "gemm"), ("gemm_kernel", "gemm"), ("splitk", "splitk"), ("attn_", "attention"),
+        ("colsum", "colsum"), ("ln_", "layernorm"), ("gn_", "groupnorm"), ("geglu", "geglu"), ("adamw", "adamw"),
+        ("sqnorm", "gradnorm"), ("at::native", "torch"), ("silu", "elementwise"), ("concat", "elementwise"),
+        ("upsample", "elementwise"), ("ddpm", "diffusion"), ("mse", "diffusion"), ("noise", "diffusion")]
+
+
+def category(name: str) -> str:
+    for key, c in CATS:
+        if key in name:
+            return c
+    return "other"
 
 
 def main():
@@ -18,7 +31,7 @@ def main():
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, stream_id, queue_id, start, end from kernels order by start").fetchall()
     marks = [r[3] for r in rows if a.marker in r[0]]
-    t0, t1 = marks[-3], marks[-2]
+    t0, t1 = marks[-4], marks[-3]   # the last timed step (bench.py runs two roofline steps after it)
     step = [r for r in rows if t0 < r[3] <= t1]
     span = (t1 - t0) / 1e6
     print(f"step span {span:.2f} ms, {len(step)} kernels")
@@ -52,6 +65,11 @@ def main():
         if before and side:
             print(f"  join: main idle {(g0 - max(r[4] for r in before)) / 1e6:.2f} ms before the grad norm; "
                   f"side stream ends {(max(r[4] for r in side) - max(r[4] for r in before)) / 1e6:.2f} ms after main's last kernel")
+    for k, v in by_stream.items():
+        cat = collections.Counter()
+        for r in v:
+            cat[category(r[0])] += r[4] - r[3]
+        print(f"  stream {k} by category: " + ", ".join(f"{n} {d / 1e6:.2f}" for n, d in cat.most_common()))
     for k, v in by_stream.items():
         agg = collections.Counter()
         for r in v:
