@@ -1,0 +1,440 @@
+// bf16 MFMA GEMM engine v2: 8 waves, 256-wide tiles, LDS-DMA staging (gfx950).
+// The kernel template; gemm2_tiles_*.hip instantiate it per tile family (parallel compilation),
+// gemm2.hip launches it.
+//
+// Same operand modes / epilogues as gemm.hip (see its header for the op -> mode table), but
+// built for the L2->CU bandwidth budget of MI355X: a 128x128 tile needs ~64 B/clk/CU of operand
+// traffic at full MFMA rate, more than the XCD L2 delivers; 256x256 halves it.
+//   * tiles 256x256 (8 waves as 2x4, 128x64 each), 256x128 or 128x256 (8 waves, 64x64 each);
+//   * operands are moved HBM/L2 -> LDS by `buffer_load_dwordx4 ... lds` (LDS-DMA): no VGPR
+//     staging, and the buffer descriptor's range check zero-fills every out-of-range lane, which
+//     is how conv padding / tile tails become zeros;
+//   * LDS images are lane-linear per 1 KiB DMA piece; the XOR swizzles that make ds_read_b128 /
+//     ds_read_b64_tr_b16 bank-conflict free are applied on the SOURCE address (rule 21);
+//   * two LDS stages, raw s_barrier, counted s_waitcnt vmcnt(N): the next tile's DMA stays in
+//     flight across the barrier while the current one is multiplied.
+#pragma once
+#include "gemm.h"
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) short4v lds_s4_t;
+#define OFF_INVALID 0x80000000u
+
+#define MEMBAR() asm volatile("" ::: "memory")
+#define BARRIER()                      \
+  do {                                 \
+    MEMBAR();                          \
+    __builtin_amdgcn_s_barrier();      \
+    MEMBAR();                          \
+  } while (0)
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One 16-byte-per-lane LDS-DMA (1 KiB per wave). Issued as inline asm on purpose: the compiler's
+// waitcnt pass cannot prove that a later ds_read of the OTHER LDS stage does not alias an
+// in-flight builtin LDS-DMA and would drain vmcnt in front of it, serialising the pipeline.
+// Ordering is owned here: every read of a stage follows wait_vmcnt<> + BARRIER on its DMA.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned off) {
+  const unsigned m0 = (unsigned)(size_t)(lds_void_t*)lds;
+  asm volatile("buffer_load_dwordx4 %1, %2, 0 offen lds" ::"{m0}"(m0), "v"(off), "s"(rs) : "memory");
+}
+
+template <int MODE> struct IsKMode {
+  static constexpr bool v = (MODE == OPM_K || MODE == OPM_CONV_FWD || MODE == OPM_CONV_DGRAD);
+};
+
+// Per-lane DMA state of one operand tile (BMN rows/cols x 64 k): BMN/8 pieces of 1 KiB, NW waves
+// take NI = BMN/(8 NW) each (piece j = wave + NW i).
+template <int MODE, int BMN, int NW>
+struct Stage {
+  static constexpr bool KM = IsKMode<MODE>::v;
+  static constexpr int NP = BMN / 8;                  // 1 KiB pieces per stage image
+  static constexpr int NI = (NP + NW - 1) / NW;       // pieces per wave (the last may be absent)
+  static constexpr bool EVEN = NP % NW == 0;          // 160-wide images: 20 pieces over 8 waves
+  static constexpr int RB = BMN * 2;      // MN-mode row bytes
+  int a[NI], b[NI], c[NI];                // K: (row elem offset | conv n,y0,x0) ; MN: (k row, col, -)
+  int t0, t1, t2;                         // K: logical chunk ; MN-conv: per-piece decode lives in a/b/c
+  bool ok[NI];
+
+  __device__ __forceinline__ void prepare(const ConvGeom& g, long long ld, int mn0, int MNsz, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = wave + NW * i;
+      if constexpr (KM) {
+        const int r = 8 * j + (lane >> 3);
+        const int gm = mn0 + r;
+        ok[i] = gm < MNsz;
+        if constexpr (MODE == OPM_K) {
+          a[i] = gm * (int)ld;
+        } else {
+          const int rr = ok[i] ? gm : 0;
+          const int hw = g.RH * g.RW;
+          const int n = rr / hw, rem = rr - n * hw;
+          const int y = rem / g.RW, x = rem - y * g.RW;
+          a[i] = n;
+          if constexpr (MODE == OPM_CONV_FWD) { b[i] = y * g.stride - g.pad; c[i] = x * g.stride - g.pad; }
+          else { b[i] = y + g.pad; c[i] = x + g.pad; }
+        }
+      } else {
+        const int byte = j * 1024 + lane * 16;
+        const int r = byte / RB;
+        const int pc = (byte % RB) >> 4;
+        const int lb = (pc >> 1) ^ mn_swz_rb<RB>(r);
+        const int col = mn0 + (lb * 2 + (pc & 1)) * 8;
+        a[i] = r;
+        ok[i] = col < MNsz;
+        if constexpr (MODE == OPM_MN || MODE == OPM_CONV_WT) {
+          b[i] = col;
+        } else {   // OPM_CONV_WGRAD: col = (tap, ch)
+          const int cc = ok[i] ? col : 0;
+          const int tap = cc / g.SC;
+          c[i] = cc - tap * g.SC;
+          b[i] = tap;
+        }
+      }
+    }
+    if constexpr (KM) t0 = (lane & 7) ^ ((lane >> 3) & 7);
+  }
+
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* img, const ConvGeom& g, long long ld, int k0,
+                                        int Kend, int wave) {
+    if constexpr (KM) {
+      const int k = k0 + 8 * t0;
+      const bool kok = k < Kend;
+      int r_ = 0, s_ = 0, ch = 0;
+      if constexpr (MODE != OPM_K) {
+        const int tap = kok ? k / g.SC : 0;
+        ch = k - tap * g.SC;
+        r_ = tap / g.KW;
+        s_ = tap - r_ * g.KW;
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        unsigned off = OFF_INVALID;
+        if constexpr (MODE == OPM_K) {
+          if (kok && ok[i]) off = (unsigned)(a[i] + k) * 2u;
+        } else {
+          bool v = kok && ok[i];
+          int sy, sx;
+          if constexpr (MODE == OPM_CONV_FWD) {
+            const int y = b[i] + r_, x = c[i] + s_;
+            if (g.upsample) { v = v && y >= 0 && y < 2 * g.SH && x >= 0 && x < 2 * g.SW; sy = y >> 1; sx = x >> 1; }
+            else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
+          } else {
+            const int ty = b[i] - r_, tx = c[i] - s_;
+            if (g.stride == 1) { sy = ty; sx = tx; }
+            else {
+              v = v && ty >= 0 && tx >= 0 && (ty % g.stride) == 0 && (tx % g.stride) == 0;
+              sy = ty / g.stride; sx = tx / g.stride;
+            }
+            v = v && sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW;
+          }
+          if (v) off = (unsigned)(((a[i] * g.SH + sy) * g.SW + sx) * (int)g.ld + ch) * 2u;
+        }
+        if (EVEN || wave + NW * i < NP) dma16(rs, img + (wave + NW * i) * 1024, off);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int k = k0 + a[i];
+        unsigned off = OFF_INVALID;
+        if constexpr (MODE == OPM_MN) {
+          if (ok[i] && k < Kend) off = (unsigned)(k * (int)ld + b[i]) * 2u;
+        } else if constexpr (MODE == OPM_CONV_WT) {   // k = tap*Cout + co -> W row co*KK + tap
+          if (ok[i] && k < Kend) {
+            const int tap = k / g.SC, co = k - tap * g.SC;
+            off = (unsigned)((co * (g.KH * g.KW) + tap) * (int)ld + b[i]) * 2u;
+          }
+        } else {   // conv wgrad: k = output pixel
+          bool v = ok[i] && k < Kend;
+          const int kk = v ? k : 0;
+          const int hw = g.RH * g.RW;
+          const int n = kk / hw, rem = kk - n * hw;
+          const int p = rem / g.RW, q = rem - p * g.RW;
+          const int tr = b[i] / g.KW, ts = b[i] - (b[i] / g.KW) * g.KW;
+          const int y = p * g.stride - g.pad + tr, x = q * g.stride - g.pad + ts;
+          int sy, sx;
+          if (g.upsample) { v = v && y >= 0 && y < 2 * g.SH && x >= 0 && x < 2 * g.SW; sy = y >> 1; sx = x >> 1; }
+          else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
+          if (v) off = (unsigned)(((n * g.SH + sy) * g.SW + sx) * (int)g.ld + c[i]) * 2u;
+        }
+        if (EVEN || wave + NW * i < NP) dma16(rs, img + (wave + NW * i) * 1024, off);
+      }
+    }
+  }
+};
+
+// fragment of a 16x16x32 operand: lane holds X[mnb + (lane&15)][kb + 8*(lane>>4) + j]
+__device__ __forceinline__ bf16x8 frag_k2(const char* img, int mnb, int kb) {
+  const int lane = threadIdx.x & 63;
+  const int row = mnb + (lane & 15);
+  return *reinterpret_cast<const bf16x8*>(img + kimg_off(row, (kb >> 3) + (lane >> 4)));
+}
+template <int RB>
+__device__ __forceinline__ int mn_off(int k, int col) {
+  return k * RB + ((((col >> 4)) ^ mn_swz_rb<RB>(k)) << 5) + ((col & 15) << 1);
+}
+template <int RB>
+__device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k0 = kb + 8 * g + q;
+  const int col = mnb + 4 * p;
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + mn_off<RB>(k0, col)));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + mn_off<RB>(k0 + 4, col)));
+  short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// NW = 8: 2 waves/SIMD (<= 256 VGPRs), wave tiles 128x64 / 64x64.  NW = 4: 1 wave/SIMD (512-entry
+// unified VGPR/AGPR file), 256x256 as 2x2 wave tiles of 128x128 -- a third less LDS read traffic
+// per MFMA (one 16x16x32 fragment read per 4 MFMAs instead of per 2.7).
+// NS = LDS ring depth (every instance today: 2).  NS = 3 / 4 at one workgroup per CU (the ring filling up to
+// 156 KiB, NS - 1 K-steps of DMA in flight) was built and measured in round 3 for the small-M SDXL shapes:
+// no faster than two 2-stage workgroups per CU (4096x1280x1280: 23.3 vs 22.8 us for 128x160; 30.8 vs 24.0
+// for 128x128), so those shapes are not latency-bound; the instances were dropped, the ring code kept.
+template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2>
+__global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 || BN == 160)) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
+                                                                 unsigned a2_bytes, unsigned b2_bytes) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // BN = 160 (N = 320 / 640 / 1280 in 2 / 4 / 8 tiles, no padding): waves 4 x 2, wave tile (BM/4) x 80
+  constexpr int WN = NW == 4 ? 2 : ((BM == 256 && BN == 128) || BN == 160 ? 2 : 4);
+  constexpr int WM = NW / WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 16, NJ = TN / 16;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
+  constexpr int STAGE = ABYTES + BBYTES;
+  constexpr int LOADS = Stage<AM, BM, NW>::NI + Stage<BMODE, BN, NW>::NI;
+  // DMA pieces this wave issues per K-step (an image of NP pieces over NW waves: waves < NP % NW take one more)
+  constexpr int NPA = Stage<AM, BM, NW>::NP, NPB = Stage<BMODE, BN, NW>::NP;
+  static_assert(!SEG2 || NS == 2, "the LoRA second segment keeps the two-stage ring");
+  constexpr bool AK = IsKMode<AM>::v, BKm = IsKMode<BMODE>::v;
+  // per-wave DMA counts differ when an image does not split evenly: the prologue then drains fully
+  constexpr bool EVEN_LOADS = Stage<AM, BM, NW>::EVEN && Stage<BMODE, BN, NW>::EVEN && (!SEG2 || (Stage<OPM_K, BM, NW>::EVEN && Stage<BKm ? OPM_K : OPM_MN, BN, NW>::EVEN));
+  if constexpr (!SEG2 && AM <= OPM_MN && BMODE <= OPM_MN) gemm_batch_offset(args);
+
+  const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  tile_coords(wg, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * args.k_per_split;
+  const int kend = min(args.K, kbeg + args.k_per_split);
+  const int nk = (kend - kbeg + 63) / 64;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)args.A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)args.B, (short)0, (int)b_bytes, 0x00020000);
+  Stage<AM, BM, NW> sa;
+  Stage<BMODE, BN, NW> sb;
+  sa.prepare(args.ga, args.lda, m0, args.M, wave, lane);
+  sb.prepare(args.gb, args.ldb, n0, args.N, wave, lane);
+  // second K segment: A2 always K-mode; B2 in the LDS image mode of B
+  constexpr int B2M = BKm ? OPM_K : OPM_MN;
+  Stage<OPM_K, SEG2 ? BM : 64 * NW / 8, NW> sa2;
+  Stage<B2M, SEG2 ? BN : 64 * NW / 8, NW> sb2;
+  __amdgpu_buffer_rsrc_t ra2 = ra, rb2 = rb;
+  if constexpr (SEG2) {
+    ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)args.A2, (short)0, (int)a2_bytes, 0x00020000);
+    rb2 = __builtin_amdgcn_make_buffer_rsrc((void*)args.B2, (short)0, (int)b2_bytes, 0x00020000);
+    sa2.prepare(args.ga, args.lda2, m0, args.M, wave, lane);
+    sb2.prepare(args.gb, args.ldb2, n0, args.N, wave, lane);
+  }
+  // K tile at k0 (never straddles K1: K1 % 64 == 0) into the stage at img
+  auto issue_tile = [&](char* img, int k0) {
+    if (!SEG2 || k0 < args.K1) {
+      sa.issue(ra, img, args.ga, args.lda, k0, SEG2 ? args.K1 : kend, wave);
+      sb.issue(rb, img + ABYTES, args.gb, args.ldb, k0, SEG2 ? args.K1 : kend, wave);
+    } else {
+      sa2.issue(ra2, img, args.ga, args.lda2, k0 - args.K1, args.K2, wave);
+      sb2.issue(rb2, img + ABYTES, args.gb, args.ldb2, k0 - args.K1, args.K2, wave);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  float4v acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  // fragment loaders (h selects the 32-wide half of the 64-deep K tile)
+  auto load_a = [&](bf16x8 (&f)[MI], const char* ia, int h) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) f[i] = AK ? frag_k2(ia, wm * TM + i * 16, 32 * h) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 32 * h);
+  };
+  auto load_b = [&](bf16x8 (&f)[NJ], const char* ib, int h) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) f[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 32 * h) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 32 * h);
+  };
+  auto mfma_block = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+  };
+  // interleave the next fragment reads into the current MFMA block: {2 MFMA, reads of 1 fragment} x (MI+NJ)
+  // (128x128: 8 MFMAs per half for 6 fragment reads -> {1 MFMA, reads} x 6, then the rest)
+  constexpr int NR = MI + NJ;
+  constexpr int PER = (MI * NJ) / NR >= 2 ? 2 : 1;
+  constexpr int REST = MI * NJ - PER * NR;
+  auto interleave = [&]() {
+#pragma unroll
+    for (int t = 0; t < NR; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, AK && BKm ? 1 : 2, 0);
+    }
+    if constexpr (REST > 0) __builtin_amdgcn_sched_group_barrier(0x008, REST, 0);
+  };
+
+  // Pipeline, ONE barrier per K-step:
+  //   phase A: MFMA(h0 of tile k) || ds_read(h1 of tile k)
+  //   wait DMA(tile k+1); barrier  -- RAW for tile k+1, WAR for tile k's stage (all its reads retired)
+  //   DMA(tile k+2) -> stage of tile k
+  //   phase B: MFMA(h1 of tile k) || ds_read(h0 of tile k+1)
+  bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
+  // this wave's DMA count per K-step (a wave-uniform value)
+  const int my_loads = (NPA / NW + (wave < NPA % NW ? 1 : 0)) + (NPB / NW + (wave < NPB % NW ? 1 : 0));
+  // wait until at most `tiles` younger K-steps' DMA of this wave are in flight (tiles <= NS - 1)
+  auto wait_tiles = [&](int tiles) {
+    if constexpr (NS == 2) {
+      (void)tiles;
+      wait_vmcnt<0>();
+    } else if constexpr (EVEN_LOADS && NPA % NW == 0 && NPB % NW == 0) {
+      if (tiles >= 3) wait_vmcnt<3 * LOADS>();
+      else if (tiles == 2) wait_vmcnt<2 * LOADS>();
+      else if (tiles == 1) wait_vmcnt<LOADS>();
+      else wait_vmcnt<0>();
+    } else {   // uneven images: this wave's count is LOADS or LOADS - 1 (or less); wait per class
+      constexpr int LO = NPA / NW + NPB / NW;
+      const int extra = my_loads - LO;   // 0, 1 or 2
+      if (tiles <= 0) wait_vmcnt<0>();
+      else if (tiles == 1) { if (extra == 0) wait_vmcnt<LO>(); else if (extra == 1) wait_vmcnt<LO + 1>(); else wait_vmcnt<LO + 2>(); }
+      else if (tiles == 2) { if (extra == 0) wait_vmcnt<2 * LO>(); else if (extra == 1) wait_vmcnt<2 * LO + 2>(); else wait_vmcnt<2 * LO + 4>(); }
+      else { if (extra == 0) wait_vmcnt<3 * LO>(); else if (extra == 1) wait_vmcnt<3 * LO + 3>(); else wait_vmcnt<3 * LO + 6>(); }
+    }
+  };
+  if (nk > 0) {
+    if constexpr (NS == 2) {
+      issue_tile(smem, kbeg);
+      if (nk > 1) {
+        issue_tile(smem + STAGE, kbeg + 64);
+        if constexpr (EVEN_LOADS) wait_vmcnt<LOADS>();
+        else wait_vmcnt<0>();
+      } else {
+        wait_vmcnt<0>();
+      }
+    } else {
+#pragma unroll
+      for (int st = 0; st < NS; ++st)
+        if (st < nk) issue_tile(smem + st * STAGE, kbeg + st * 64);
+      wait_tiles(min(NS, nk) - 1);   // tile 0 has landed
+    }
+    BARRIER();
+    load_b(fb0, smem + ABYTES, 0);
+    load_a(fa0, smem, 0);
+  }
+  int stg = 0;   // ring slot of tile kt (kt % NS)
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* ia = smem + stg * STAGE;
+    const char* ib = ia + ABYTES;
+    const int nstg = stg + 1 == NS ? 0 : stg + 1;
+    // phase A
+    __builtin_amdgcn_sched_barrier(0);
+    load_b(fb1, ib, 1);
+    load_a(fa1, ia, 1);
+    mfma_block(fa0, fb0);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // tile kt+1 has landed: the tiles after it that may still be in flight are kt+2 .. min(kt+NS-1, nk-1)
+    wait_tiles(min(NS - 2, nk - kt - 2));
+    BARRIER();
+    if (kt + NS < nk) issue_tile(smem + stg * STAGE, kbeg + (kt + NS) * 64);   // refill tile kt's slot
+    // phase B
+    __builtin_amdgcn_sched_barrier(0);
+    {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
+      const char* na = smem + nstg * STAGE;
+      load_b(fb0, na + ABYTES, 0);
+      load_a(fa0, na, 0);
+      mfma_block(fa1, fb1);
+      interleave();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    stg = nstg;
+  }
+
+  const bool use_slab = gridDim.z > 1;
+  const int g = lane >> 4;
+  if (use_slab || gemm_wide_ok(args)) {
+    // Row blocks (i, i+1) of one column block exchange lane groups with v_permlane16_swap:
+    // afterwards lane group g holds 8 consecutive columns 8(g>>1).. of row block i + (g&1).
+#pragma unroll
+    for (int i = 0; i < MI; i += 2) {
+      const int m = m0 + wm * TM + (i + (g & 1)) * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][t]), __float_as_uint(acc[i + 1][j][t]),
+                                                          false, false);
+          v[t] = __uint_as_float(r[0]);
+          v[4 + t] = __uint_as_float(r[1]);
+        }
+        const int n = n0 + wn * TN + j * 16 + 8 * (g >> 1);
+        if (m >= args.M || n >= args.N) continue;
+        if (n + 8 <= args.N) {
+          gemm_store8(args, m, n, v, split, use_slab);
+        } else {
+          float v4[4] = {v[0], v[1], v[2], v[3]};
+          gemm_store4(args, m, n, v4, split, use_slab);
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = m0 + wm * TM + i * 16 + (lane & 15);
+    if (m >= args.M) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * TN + j * 16 + 4 * g;
+      if (n >= args.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      gemm_store4(args, m, n, v, split, use_slab);
+    }
+  }
+}
+
+typedef void (*gemm2_fn)(GemmArgs, unsigned, unsigned, unsigned, unsigned);
+
+template <int BM, int BN, int NW, int NS = 2>
+static gemm2_fn pick2(int am, int bm, bool seg2) {
+  if (seg2) {   // LoRA-fused forms: linear fwd, conv fwd, linear dgrad
+    if constexpr (NS != 2) return nullptr;
+    if (am == OPM_K && bm == OPM_K) return gemm2_kernel<OPM_K, OPM_K, BM, BN, NW, true>;
+    if (am == OPM_CONV_FWD && bm == OPM_K) return gemm2_kernel<OPM_CONV_FWD, OPM_K, BM, BN, NW, true>;
+    if (am == OPM_K && bm == OPM_MN) return gemm2_kernel<OPM_K, OPM_MN, BM, BN, NW, true>;
+    return nullptr;
+  }
+#define CASE2(a, b) if (am == a && bm == b) return gemm2_kernel<a, b, BM, BN, NW, false, NS>;
+  CASE2(OPM_K, OPM_K)
+  CASE2(OPM_K, OPM_MN)
+  CASE2(OPM_MN, OPM_MN)
+  CASE2(OPM_MN, OPM_K)
+  CASE2(OPM_CONV_FWD, OPM_K)
+  CASE2(OPM_CONV_DGRAD, OPM_K)
+  CASE2(OPM_CONV_DGRAD, OPM_CONV_WT)
+  CASE2(OPM_MN, OPM_CONV_WGRAD)
+#undef CASE2
+  return nullptr;
+}
+

@@ -141,8 +141,8 @@ def test_autotuned_plans(dev, autotune):
 @pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_every_tile_explicit(dev, tile, monkeypatch):
     """every engine tile (4 = 128x128 with 8 waves, 2 workgroups per CU; 5 / 6 = 128x64 / 64x128; 7 / 8 = 128x160 /
-    256x160, 20 DMA pieces over 8 waves and 320-byte MN rows) through otamd_gemm_explicit:
-    linear fwd (+bias +residual), dgrad, wgrad (split-K) and conv fwd / dgrad / wgrad, ragged sizes."""
+    256x160, 20 DMA pieces over 8 waves and 320-byte MN rows) through otamd_gemm_explicit: linear fwd (+bias +residual), dgrad, wgrad (split-K),
+    conv fwd / dgrad / wgrad, ragged sizes, and K of 1 to 5 K-steps (ring prologue and tail wait counts)."""
     torch.manual_seed(11)
     splits = {"v": 1}
 
@@ -165,6 +165,11 @@ def test_every_tile_explicit(dev, tile, monkeypatch):
         splits["v"] = sp
         close(K.linear_wgrad(dy, x), dy.float().t() @ x.float(), tol=1e-2)
     splits["v"] = 1
+    for kd in (64, 72, 136, 200, 320):     # 1, 2, 3, 4, 5 K-steps
+        xs, ws_ = rnd(300, kd, dev=dev), rnd(200, kd, dev=dev, scale=0.05)
+        close(K.linear(xs, ws_), xs.float() @ ws_.float().t())
+        dys = rnd(300, 200, dev=dev)
+        close(K.linear_dgrad(dys, ws_[:, :kd]), dys.float() @ ws_.float())
     xc = rnd(2, 24, 20, 64, dev=dev)
     wc = rnd(96, 3, 3, 64, dev=dev, scale=0.05)
     yc = K.conv2d(xc, wc, pad=1)
