@@ -54,6 +54,12 @@ typedef struct GemmArgs {
      (z / bdiv) * s0 + (z % bdiv) * s1 elements ((image, head) pairs of [B, N, H*D] activations) */
   int batch, bdiv;
   long long sa0, sa1, sb0, sb1, sc0, sc1;
+  /* optional column sums of an MN-mode A over the K range (the bias gradient of a Linear / conv weight
+     gradient dW = dY^T X: colsum[m] = sum_k dY[k][m], replaces the separate dY.sum(0) of autograd):
+     bf16 or fp32 [M], overwritten or accumulated; with split-K the partials go to the workspace after the
+     GEMM slabs (splits * M floats) and the split-K reduce folds them */
+  void* colsum; int colsum_f32; int colsum_acc;
+  float* colsum_slab;
 } GemmArgs;
 
 typedef struct AttnArgs {
@@ -103,6 +109,8 @@ int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspac
 /* replaces: (diagnostic) the tile otamd_gemm launches for these arguments: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256, 3 256x256/4 waves,
    4 128x128, 5 128x64, 6 64x128, 7 128x160, 8 256x160 */
 int otamd_gemm_plan_tile(const GemmArgs* in, int splits);
+/* workspace bytes of a `splits`-way split-K launch (fp32 slabs, + the column-sum partials when colsum is set) */
+long long otamd_gemm_ws_bytes(const GemmArgs* in, int splits);
 
 /* replaces: ABI check */
 int otamd_gemm_args_size(void);

@@ -33,7 +33,8 @@ class GemmArgs(C.Structure):
                 ("A2", C.c_void_p), ("lda2", C.c_longlong), ("B2", C.c_void_p), ("ldb2", C.c_longlong),
                 ("K1", C.c_int), ("K2", C.c_int),
                 ("batch", C.c_int), ("bdiv", C.c_int), ("sa0", C.c_longlong), ("sa1", C.c_longlong),
-                ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong)]
+                ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong),
+                ("colsum", C.c_void_p), ("colsum_f32", C.c_int), ("colsum_acc", C.c_int), ("colsum_slab", C.c_void_p)]
 
 
 class AdamwGroup(C.Structure):
@@ -84,6 +85,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_gemm_plan": [C.POINTER(GemmArgs), I, C.POINTER(C.c_int)],
     "otamd_gemm_explicit": [C.POINTER(GemmArgs), I, I, VP, LL, VP],
     "otamd_gemm_plan_tile": [C.POINTER(GemmArgs), I],
+    "otamd_gemm_ws_bytes": [C.POINTER(GemmArgs), I],
     "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_bf16_range": [VP, VP, VP, VP, LL, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],

@@ -80,6 +80,10 @@ __device__ __forceinline__ float dgelu_f(float x) {
 
 // 8 bf16 in one 16-byte register tuple
 struct __align__(16) bf8 { uint32_t w[4]; };
+// make the compiler treat v as freshly produced (no reuse of values derived from it before this point)
+__device__ __forceinline__ void opaque(bf8& v) {
+  asm volatile("" : "+v"(v.w[0]), "+v"(v.w[1]), "+v"(v.w[2]), "+v"(v.w[3]));
+}
 __device__ __forceinline__ void unpack8(const bf8& v, float* f) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {

@@ -40,6 +40,11 @@ struct GemmArgs {
   // [B, N, H*D] activation are bdiv = H, s0 = batch stride, s1 = D.  batch <= 1: unbatched.
   int batch, bdiv;
   long long sa0, sa1, sb0, sb1, sc0, sc1;
+  // column sums of the MN-mode A over the K range (wgrad: the bias gradient sum_k dY[k][m]) -- colsum bf16 /
+  // f32 [M], overwrite or accumulate; split-K: per-split partials in colsum_slab [splits][M], folded by the
+  // split-K reduce.  v2 tiles only; tile-column 0 workgroups accumulate them from the LDS image of A.
+  void* colsum; int colsum_f32; int colsum_acc;
+  float* colsum_slab;
 };
 
 __device__ __forceinline__ void gemm_batch_offset(GemmArgs& a) {

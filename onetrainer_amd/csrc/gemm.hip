@@ -289,6 +289,19 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs args, int s
     const unsigned m = i / NV, n = (i - m * NV) * V;
     splitk_combine<V>(args, m, n, splits);
   }
+  if (args.colsum) {   // the fused column sums' per-split partials, summed in split order
+    for (unsigned m = blockIdx.x * 256u + threadIdx.x; m < (unsigned)args.M; m += gridDim.x * 256u) {
+      float t = args.colsum_slab[m];
+      for (int z = 1; z < splits; ++z) t += args.colsum_slab[(long long)z * args.M + m];
+      if (args.colsum_f32) {
+        float* d = reinterpret_cast<float*>(args.colsum) + m;
+        *d = args.colsum_acc ? *d + t : t;
+      } else {
+        bf16_t* d = reinterpret_cast<bf16_t*>(args.colsum) + m;
+        *d = f2bf(args.colsum_acc ? bf2f(*d) + t : t);
+      }
+    }
+  }
 }
 
 typedef void (*gemm_fn)(GemmArgs);
@@ -390,6 +403,13 @@ static GemmPlan plan_gemm(int M, int N, int K, int max_splits, bool v2_only = fa
   return best;
 }
 
+// workspace bytes a `splits`-way split-K launch needs: the fp32 C slabs [splits][M][N] and, with fused
+// column sums, their partials [splits][M] after them
+OTAMD_API long long otamd_gemm_ws_bytes(const GemmArgs* in, int splits) {
+  if (!in || splits <= 1) return 0;
+  return (long long)splits * in->M * in->N * 4 + (in->colsum ? (long long)splits * in->M * 4 : 0);
+}
+
 // C-ABI.  Preconditions (checked, OTAMD_EINVAL otherwise): M,N,K > 0; N % 4 == 0; K-mode
 // operands need K % 8 == 0, MN-mode operands MN % 8 == 0; leading dims multiples of 8
 // elements; base pointers 16-byte aligned; conv gathers need SC % 8 == 0.
@@ -401,7 +421,7 @@ OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_
   if (in->batch > 1) s = 1;
   if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT || in->A2 != nullptr).splits;
   if (splits_out) *splits_out = s;
-  return s > 1 ? (long long)s * in->M * in->N * 4 : 0;
+  return s > 1 ? otamd_gemm_ws_bytes(in, s) : 0;
 }
 
 static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_only);
@@ -476,18 +496,22 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   splits = (int)((a.K + kps - 1) / kps);
   a.k_per_split = (int)kps;
   if (splits > 1) {
-    if (!workspace || ws_bytes < (long long)splits * a.M * a.N * 4 || !aligned16(workspace)) return OTAMD_EINVAL;
+    if (!workspace || ws_bytes < otamd_gemm_ws_bytes(&a, splits) || !aligned16(workspace)) return OTAMD_EINVAL;
     a.slab = (float*)workspace;
+    a.colsum_slab = a.colsum ? a.slab + (long long)splits * a.M * a.N : nullptr;
   } else {
     a.slab = nullptr;
+    a.colsum_slab = nullptr;
   }
+  if (a.colsum && (a.amode != OPM_MN || a.A2 || a.batch > 1)) return OTAMD_EINVAL;
   int tile = force_tile == -9 ? resolve_tile(a, splits, plan, v2_only) : force_tile;
+  if (a.colsum && (tile < 0 || tile == 3)) tile = 0;   // the fused column sums live in the 8-wave v2 kernels
   if (v2_only && tile < 0) return OTAMD_EUNSUPPORTED;
   int rc = OTAMD_EUNSUPPORTED;
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
   if (rc != OTAMD_OK) {
-    if (!fn || a.A2) return rc;   // v1 has no conv-weight B and no second K segment
+    if (!fn || a.A2 || a.colsum) return rc;   // v1 has no conv-weight B, no second K segment, no column sums
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid(tiles, a.batch > 1 ? a.batch : 1, splits);
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);

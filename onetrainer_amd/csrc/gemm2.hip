@@ -5,10 +5,10 @@
 #include <mutex>
 #include <unordered_set>
 
-gemm2_fn gemm2_pick_a(int tile, int am, int bm, bool seg2);   // 0, 3   256x256
-gemm2_fn gemm2_pick_b(int tile, int am, int bm, bool seg2);   // 1, 2   256x128, 128x256
-gemm2_fn gemm2_pick_c(int tile, int am, int bm, bool seg2);   // 4, 5, 6  128x128, 128x64, 64x128
-gemm2_fn gemm2_pick_d(int tile, int am, int bm, bool seg2);   // 7, 8   x160
+gemm2_fn gemm2_pick_a(int tile, int am, int bm, bool seg2, bool cs);   // 0, 3   256x256
+gemm2_fn gemm2_pick_b(int tile, int am, int bm, bool seg2, bool cs);   // 1, 2   256x128, 128x256
+gemm2_fn gemm2_pick_c(int tile, int am, int bm, bool seg2, bool cs);   // 4, 5, 6  128x128, 128x64, 64x128
+gemm2_fn gemm2_pick_d(int tile, int am, int bm, bool seg2, bool cs);   // 7, 8   x160
 
 // byte extent an operand's gathers may touch (the DMA descriptor's range)
 static long long operand_bytes(int mode, const bf16_t* p, long long ld, int MN, int K, const ConvGeom& g) {
@@ -27,6 +27,8 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   gemm2_fn fn = nullptr;
   int BMv = 256, BNv = 256, NWv = 8, NSv = 2;
   const bool seg2 = a.A2 != nullptr;
+  const bool cs = a.colsum != nullptr;
+  if (cs && (a.amode != OPM_MN || seg2 || a.batch > 1 || (splits > 1 && !a.colsum_slab))) return OTAMD_EUNSUPPORTED;
   unsigned a2b = 0, b2b = 0;
   if (seg2) {
     const long long x = ((long long)(a.M - 1) * a.lda2 + a.K2) * 2;
@@ -36,10 +38,10 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
     b2b = (unsigned)y;
   }
   switch (tile) {
-    case 0: case 3: fn = gemm2_pick_a(tile, a.amode, a.bmode, seg2); break;
-    case 1: case 2: fn = gemm2_pick_b(tile, a.amode, a.bmode, seg2); break;
-    case 4: case 5: case 6: fn = gemm2_pick_c(tile, a.amode, a.bmode, seg2); break;
-    case 7: case 8: fn = gemm2_pick_d(tile, a.amode, a.bmode, seg2); break;
+    case 0: case 3: fn = gemm2_pick_a(tile, a.amode, a.bmode, seg2, cs); break;
+    case 1: case 2: fn = gemm2_pick_b(tile, a.amode, a.bmode, seg2, cs); break;
+    case 4: case 5: case 6: fn = gemm2_pick_c(tile, a.amode, a.bmode, seg2, cs); break;
+    case 7: case 8: fn = gemm2_pick_d(tile, a.amode, a.bmode, seg2, cs); break;
     default: break;
   }
   // tile geometry: (BM, BN, waves, ring depth)
@@ -48,7 +50,7 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   if (tile >= 0 && tile < 9) { BMv = geo[tile][0]; BNv = geo[tile][1]; NWv = geo[tile][2]; NSv = geo[tile][3]; }
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
-  const int lds = NSv * (BMv + BNv) * 128;
+  const int lds = NSv * (BMv + BNv) * 128 + (cs && BMv == 256 ? (NWv * 64 / (BMv / 8)) * BMv * 4 : 0);
   {   // the LDS opt-in once per kernel instance (a per-launch driver call costs host time on every GEMM)
     static std::mutex mu;
     static std::unordered_set<const void*> done;

@@ -197,7 +197,17 @@ __device__ __forceinline__ bf16x8 frag_mn2(const char* img, int mnb, int kb) {
 // 156 KiB, NS - 1 K-steps of DMA in flight) was built and measured in round 3 for the small-M SDXL shapes:
 // no faster than two 2-stage workgroups per CU (4096x1280x1280: 23.3 vs 22.8 us for 128x160; 30.8 vs 24.0
 // for 128x128), so those shapes are not latency-bound; the instances were dropped, the ring code kept.
-template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2>
+// CS: also the column sums of the MN-mode A over this split's K range (GemmArgs.colsum: a weight
+// gradient's bias gradient from the dY image already in LDS).  Workgroups of tile column 0 read each
+// landed A image once more (16-byte chunks, one 64-row K-step) right after the barrier that publishes it;
+// BM = 256 tiles keep the per-thread partials in an LDS region after the ring (their register file is
+// full), smaller tiles in 8 VGPRs.  Folded in a fixed order at the end: deterministic.
+template <int BM, int RB>
+__device__ __forceinline__ int mn_chunk_off(int k, int c) {   // 16-byte chunk c (columns 8c..8c+7) of row k
+  return k * RB + ((((c >> 1)) ^ mn_swz_rb<RB>(k)) << 5) + ((c & 1) << 4);
+}
+
+template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2, bool CS = false>
 __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 || BN == 160)) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
                                                                  unsigned a2_bytes, unsigned b2_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -340,6 +350,54 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     load_b(fb0, smem + ABYTES, 0);
     load_a(fa0, smem, 0);
   }
+  // ---- column sums of A (CS) ----
+  static_assert(!CS || (AM == OPM_MN && !SEG2), "column sums of an MN-mode A, single segment");
+  constexpr int CPR = BM / 8;                       // 16-byte chunks per A-image row
+  constexpr int RG = NW * 64 / CPR;                 // row groups (threads per chunk column)
+  constexpr int NCH = 64 / RG;                      // rows of one K-step per thread
+  constexpr bool CS_LDS = BM == 256;
+  static_assert(!CS || (RG * CPR == NW * 64 && NCH * RG == 64), "colsum thread map");
+  const bool cs_on = CS && tn == 0;                 // workgroup-uniform
+  const int cs_c = threadIdx.x % CPR, cs_rg = threadIdx.x / CPR;
+  float cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = 0.f;
+  float* cs_lds = reinterpret_cast<float*>(smem + NS * STAGE) + (cs_rg * BM + cs_c * 8);
+  auto colsum_tile = [&](const char* ia) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const bf8 v = *reinterpret_cast<const bf8*>(ia + mn_chunk_off<BM, BM * 2>(cs_rg + RG * i, cs_c));
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] += f[j];
+    }
+    if constexpr (CS_LDS) {
+      float4* q = reinterpret_cast<float4*>(cs_lds);
+      float4 a0 = q[0], a1 = q[1];
+      a0.x += t[0]; a0.y += t[1]; a0.z += t[2]; a0.w += t[3];
+      a1.x += t[4]; a1.y += t[5]; a1.z += t[6]; a1.w += t[7];
+      q[0] = a0;
+      q[1] = a1;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] += t[j];
+    }
+  };
+  if constexpr (CS) {
+    if (cs_on && nk > 0) {
+      if constexpr (CS_LDS) {
+        float4* q = reinterpret_cast<float4*>(cs_lds);
+        q[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        q[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      colsum_tile(smem);   // tile 0 (published by the prologue barrier)
+    }
+  }
+
   int stg = 0;   // ring slot of tile kt (kt % NS)
   for (int kt = 0; kt < nk; ++kt) {
     const char* ia = smem + stg * STAGE;
@@ -357,6 +415,10 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     wait_tiles(min(NS - 2, nk - kt - 2));
     BARRIER();
     if (kt + NS < nk) issue_tile(smem + stg * STAGE, kbeg + (kt + NS) * 64);   // refill tile kt's slot
+    if constexpr (CS) {   // tile kt+1: published by this barrier, refilled only after the next one
+      __builtin_amdgcn_sched_barrier(0);
+      if (cs_on && kt + 1 < nk) colsum_tile(smem + nstg * STAGE);
+    }
     // phase B
     __builtin_amdgcn_sched_barrier(0);
     {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
@@ -371,6 +433,34 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
   }
 
   const bool use_slab = gridDim.z > 1;
+  if constexpr (CS) {
+    if (cs_on) {   // fold the row groups in a fixed order; tile column 0 only (workgroup-uniform branch)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      BARRIER();   // every wave past its last ring read (and, for CS_LDS, its last partial update)
+      float* red = reinterpret_cast<float*>(smem + (CS_LDS ? NS * STAGE : 0));
+      if constexpr (!CS_LDS) {
+        float4* q = reinterpret_cast<float4*>(red + cs_rg * BM + cs_c * 8);
+        q[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        q[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+        BARRIER();
+      }
+      for (int c = threadIdx.x; c < BM; c += NW * 64) {
+        float tot = 0.f;
+        for (int r = 0; r < RG; ++r) tot += red[r * BM + c];
+        const int m = m0 + c;
+        if (m < args.M) {
+          if (use_slab) args.colsum_slab[(long long)split * args.M + m] = tot;
+          else if (args.colsum_f32) {
+            float* d = reinterpret_cast<float*>(args.colsum) + m;
+            *d = args.colsum_acc ? *d + tot : tot;
+          } else {
+            bf16_t* d = reinterpret_cast<bf16_t*>(args.colsum) + m;
+            *d = f2bf(args.colsum_acc ? bf2f(*d) + tot : tot);
+          }
+        }
+      }
+    }
+  }
   const int g = lane >> 4;
   if (use_slab || gemm_wide_ok(args)) {
     // Row blocks (i, i+1) of one column block exchange lane groups with v_permlane16_swap:
@@ -417,7 +507,15 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
 typedef void (*gemm2_fn)(GemmArgs, unsigned, unsigned, unsigned, unsigned);
 
 template <int BM, int BN, int NW, int NS = 2>
-static gemm2_fn pick2(int am, int bm, bool seg2) {
+static gemm2_fn pick2(int am, int bm, bool seg2, bool cs = false) {
+  if (cs) {   // weight gradients with the bias gradient fused: MN-mode A (dY), linear or conv B
+    if constexpr (NW == 8) {
+      if (seg2) return nullptr;
+      if (am == OPM_MN && bm == OPM_MN) return gemm2_kernel<OPM_MN, OPM_MN, BM, BN, NW, false, NS, true>;
+      if (am == OPM_MN && bm == OPM_CONV_WGRAD) return gemm2_kernel<OPM_MN, OPM_CONV_WGRAD, BM, BN, NW, false, NS, true>;
+    }
+    return nullptr;
+  }
   if (seg2) {   // LoRA-fused forms: linear fwd, conv fwd, linear dgrad
     if constexpr (NS != 2) return nullptr;
     if (am == OPM_K && bm == OPM_K) return gemm2_kernel<OPM_K, OPM_K, BM, BN, NW, true>;

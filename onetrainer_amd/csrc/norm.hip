@@ -673,6 +673,12 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(const bf16_t* __restri
   // partial row groups: rows past the end returned above, so every lane of a live group is live
   const float m1 = group_sum(s1, L) / C, m2 = group_sum(s2, L) / C;
 #pragma unroll
+  for (int k = 0; k < CPL; ++k) {   // re-unpack below rather than keep the first pass's floats live
+    opaque(xr[k]);
+    opaque(dr[k]);
+    if (add) opaque(ar[k]);
+  }
+#pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int c8 = li + L * k;
     float xf[8], dv[8], gm[8], o[8];

@@ -84,6 +84,13 @@ def _tune_key(a: GemmArgs) -> tuple:
             bool(a.residual), bool(a.accumulate), a.ga.KH, a.ga.stride, a.ga.upsample, a.gb.KH)
 
 
+def _ws_bytes(a: GemmArgs, s: int) -> int:
+    """workspace of an s-way split-K launch (otamd_gemm_ws_bytes): fp32 slabs + fused column-sum partials."""
+    if s <= 1:
+        return 0
+    return s * a.M * a.N * 4 + (s * a.M * 4 if a.colsum else 0)
+
+
 def _tune(a: GemmArgs, device) -> tuple:
     v2_only = a.bmode == OPM_CONV_WT or bool(a.A2)   # conv-weight B / second K segment: v2 kernels only
     torch.cuda.synchronize(device)
@@ -95,6 +102,9 @@ def _tune(a: GemmArgs, device) -> tuple:
         scratch = torch.empty(int(a.sc0 * (a.batch // max(1, a.bdiv)) + a.sc1 * a.bdiv + a.M * a.ldc) * esz + 256,
                               dtype=torch.uint8, device=device)
     b.C = _p(scratch)
+    if a.colsum:   # the candidates write their column sums to scratch too (never into the real bias gradient)
+        cs_scratch = torch.empty(a.M, dtype=torch.float32, device=device)
+        b.colsum, b.colsum_f32, b.colsum_acc = _p(cs_scratch), 1, 0
     best, best_t, seen = None, float("inf"), set()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for s in (_SPLITS if a.batch <= 1 else (1,)):
@@ -103,7 +113,7 @@ def _tune(a: GemmArgs, device) -> tuple:
         if se in seen or (s > 1 and kps < 256):
             continue
         seen.add(se)
-        ws_bytes = se * a.M * a.N * 4 if se > 1 else 0
+        ws_bytes = _ws_bytes(a, se)
         ws = workspace(ws_bytes, device) if ws_bytes else None
         for t in _TILES:
             if v2_only and t < 0:
@@ -193,7 +203,7 @@ def _gemm(a: GemmArgs, splits: int, device) -> None:
         ov = _PLAN_OVERRIDES.get((a.amode, a.bmode, a.M, a.N, a.K))
         if ov is not None:
             t, s = ov
-            ws_bytes = s * a.M * a.N * 4 if s > 1 else 0
+            ws_bytes = _ws_bytes(a, s)
             ws = workspace(ws_bytes, device) if ws_bytes else None
             check(lib().otamd_gemm_explicit(C.byref(a), t, s, _p(ws), ws_bytes, stream_handle()), "otamd_gemm_explicit")
             return
@@ -209,7 +219,7 @@ def _gemm(a: GemmArgs, splits: int, device) -> None:
         plan = _plan_table().get(_tune_key(a))
     if plan is not None:
         t, s = plan
-        ws_bytes = s * a.M * a.N * 4 if s > 1 else 0
+        ws_bytes = _ws_bytes(a, s)
         ws = workspace(ws_bytes, device) if ws_bytes else None
         check(lib().otamd_gemm_explicit(C.byref(a), t, s, _p(ws), ws_bytes, stream_handle()), "otamd_gemm_explicit")
         return
@@ -329,9 +339,18 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, acc
     return out
 
 
+def _bias_grad(a: GemmArgs, bias_grad, bias_acc: bool, n: int):
+    """fuse the bias gradient sum_t dy[t, :] into a weight-gradient GEMM (GemmArgs.colsum)."""
+    if bias_grad is not None:
+        _req(bias_grad.numel() == n and bias_grad.is_contiguous() and bias_grad.dtype in (BF16, F32), "bias grad [N]")
+        a.colsum, a.colsum_f32, a.colsum_acc = _p(bias_grad), int(bias_grad.dtype == F32), int(bias_acc)
+
+
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out=None, accumulate=False, splits=None,
-                 alpha=1.0) -> torch.Tensor:
-    """dw[N,K] = alpha * dy[T,N]^T @ x[T,K]  (split-K over tokens T, deterministic slab reduce)."""
+                 alpha=1.0, bias_grad=None, bias_acc=False) -> torch.Tensor:
+    """dw[N,K] = alpha * dy[T,N]^T @ x[T,K]  (split-K over tokens T, deterministic slab reduce).
+    bias_grad [N]: also db = sum_t dy[t, :] (unscaled; overwritten or, bias_acc, accumulated), from the dy
+    image the GEMM already stages (no second pass over dy)."""
     _req(dy.dtype == BF16 and x.dtype == BF16, "linear_wgrad: bf16")
     T, N = dy.shape
     T2, K = x.shape
@@ -342,6 +361,7 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out=None, accumulate=False, 
     a.B, a.ldb, a.bmode = _p(x), _ld_rows(x), OPM_MN
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), out.stride(0), int(out.dtype == F32), int(accumulate)
     a.M, a.N, a.K, a.alpha = N, K, T, alpha
+    _bias_grad(a, bias_grad, bias_acc, N)
     _gemm(a, splits or 0, dy.device)
     return out
 
@@ -428,8 +448,9 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw, stride=1, pad=1, out=
 
 
 def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ksize=3, stride=1, pad=1, upsample=False, out=None,
-                 accumulate=False, splits=None) -> torch.Tensor:
-    """dw[co,r,s,ci] = sum_{n,p,q} dy[n,p,q,co] * x[n, p*st+r-pad, q*st+s-pad, ci]."""
+                 accumulate=False, splits=None, bias_grad=None, bias_acc=False) -> torch.Tensor:
+    """dw[co,r,s,ci] = sum_{n,p,q} dy[n,p,q,co] * x[n, p*st+r-pad, q*st+s-pad, ci]; bias_grad [Cout]: also
+    db = sum_{n,p,q} dy[n,p,q,:] fused into the same GEMM."""
     N, P, Q, Cout, ldy = _nhwc(dy)
     N2, H, W, Cin, ldx = _nhwc(x)
     _req(N == N2 and conv_out_hw(H, W, ksize, stride, pad, upsample) == (P, Q), "wgrad geometry")
@@ -443,6 +464,7 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ksize=3, stride=1, pad=1, up
     a.C, a.ldc, a.c_f32, a.accumulate = _p(out), ksize * ksize * Cin, int(out.dtype == F32), int(accumulate)
     Kg = N * P * Q
     a.M, a.N, a.K = Cout, ksize * ksize * Cin, Kg
+    _bias_grad(a, bias_grad, bias_acc, Cout)
     _gemm(a, splits or 0, dy.device)
     return out
 

@@ -84,9 +84,10 @@ class RowsLinearFn(torch.autograd.Function):
                         for p, (g, (n0, n1)) in enumerate(zip(site.g_up, site.ranges)):
                             K.linear_wgrad(dys[:, n0:n1], t[:, p * rk:(p + 1) * rk], out=g, accumulate=acc,
                                            alpha=site.scale)
-                    if wref.trainable:
-                        K.linear_wgrad(dys, xs, out=wref.g, accumulate=wref.acc())
-                    if btr:
+                    if wref.trainable:   # bias gradient fused into the weight-gradient GEMM
+                        K.linear_wgrad(dys, xs, out=wref.g, accumulate=wref.acc(),
+                                       bias_grad=bref.g.view(-1) if btr else None, bias_acc=btr and bref.acc())
+                    elif btr:
                         K.colsum(dys, out=bref.g.view(1, -1), accumulate=bref.acc())
             if dx is not None:
                 if site is not None:

@@ -94,9 +94,10 @@ class LinearFn(torch.autograd.Function):
         btr = bref is not None and bref.trainable
         if wref.trainable or btr:
             with S.wgrad_region((dy2, x2)):       # weight gradients overlap the dgrad chain
-                if wref.trainable:
-                    K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
-                if btr:
+                if wref.trainable:   # the bias gradient (sum of dy over tokens) rides in the same GEMM
+                    K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc(),
+                                   bias_grad=bref.g.view(-1) if btr else None, bias_acc=btr and bref.acc())
+                elif btr:
                     K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
         dx = None
         if ctx.needs_input_grad[0]:
@@ -224,9 +225,10 @@ class ConvFn(torch.autograd.Function):
         btr = bref is not None and bref.trainable
         if wref.trainable or btr:
             with S.wgrad_region((dy, x)):
-                if wref.trainable:
-                    K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc())
-                if btr:
+                if wref.trainable:   # + the bias gradient from the same GEMM's dy images
+                    K.conv2d_wgrad(dy, x, 3, ctx.stride, 1, upsample=ctx.upsample, out=wref.g, accumulate=wref.acc(),
+                                   bias_grad=bref.g.view(-1) if btr else None, bias_acc=btr and bref.acc())
+                elif btr:
                     K.colsum(dy, out=bref.g.view(1, -1), accumulate=bref.acc())
         dx = None
         if ctx.needs_input_grad[0]:

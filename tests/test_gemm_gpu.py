@@ -148,7 +148,7 @@ def test_every_tile_explicit(dev, tile, monkeypatch):
 
     def explicit(a, s_, device):
         sp = splits["v"]
-        ws_bytes = sp * a.M * a.N * 4 if sp > 1 else 0
+        ws_bytes = K._ws_bytes(a, sp)
         ws = K.workspace(ws_bytes, device) if ws_bytes else None
         rc = K.lib().otamd_gemm_explicit(C.byref(a), tile, sp, K._p(ws), ws_bytes, K.stream_handle())
         if rc == 3 and tile in (-1, 3):   # OTAMD_EUNSUPPORTED: v1 has no conv-weight B, 4-wave tile has no 2nd segment
@@ -164,6 +164,13 @@ def test_every_tile_explicit(dev, tile, monkeypatch):
     for sp in (1, 3):
         splits["v"] = sp
         close(K.linear_wgrad(dy, x), dy.float().t() @ x.float(), tol=1e-2)
+        if tile not in (-1, 3):   # fused bias gradient (GemmArgs.colsum; 4-wave / v1 tiles remap to tile 0)
+            db = torch.full((328,), 0.5, dtype=BF, device=dev)
+            close(K.linear_wgrad(dy, x, bias_grad=db, bias_acc=True), dy.float().t() @ x.float(), tol=1e-2)
+            close(db, dy.float().sum(0) + 0.5, tol=1e-2)
+            db32 = torch.empty(328, device=dev)
+            K.linear_wgrad(dy, x, bias_grad=db32)
+            close(db32, dy.float().sum(0), tol=2e-3)
     splits["v"] = 1
     for kd in (64, 72, 136, 200, 320):     # 1, 2, 3, 4, 5 K-steps
         xs, ws_ = rnd(300, kd, dev=dev), rnd(200, kd, dev=dev, scale=0.05)
@@ -178,5 +185,11 @@ def test_every_tile_explicit(dev, tile, monkeypatch):
         dxc = K.conv2d_dgrad(yc, wc, (24, 20), 1, 1)
         refd = torch.nn.grad.conv2d_input(nchw(xc).shape, wc.permute(0, 3, 1, 2).float(), nchw(yc), padding=1)
         close(dxc, to_nhwc(refd))
+    if tile not in (-1, 3):   # conv weight gradient with the fused bias gradient
+        dbc = torch.empty(96, device=dev)
+        dwc = K.conv2d_wgrad(yc, xc, 3, 1, 1, bias_grad=dbc)
+        refw = torch.nn.grad.conv2d_weight(nchw(xc), (96, 64, 3, 3), nchw(yc), padding=1)
+        close(dwc, refw.permute(0, 2, 3, 1), tol=2e-2)
+        close(dbc, yc.float().sum((0, 1, 2)), tol=2e-3)
 
 
