@@ -198,6 +198,13 @@ int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long 
                         const float* a, const float* b, void* dgamma, void* dbeta, int param_f32, int param_acc,
                         float* ws, int accumulate, hipStream_t stream);
 
+/* replaces: autograd of GroupNorm(+SiLU) plus the autograd add of its input's second gradient (the
+   ResnetBlock2D shortcut / Transformer2DModel proj_out residual): dx = GroupNorm-backward(dy) + dres */
+int otamd_groupnorm_bwd_res(const void* x, long long ldx, const void* dy, long long lddy, const void* dres,
+                            long long ldres, void* dx, long long lddx, int N, int HW, int C, int G, const void* gamma,
+                            int silu, const float* mean, const float* rstd, const float* a, const float* b,
+                            void* dgamma, void* dbeta, int param_f32, int param_acc, float* ws, hipStream_t stream);
+
 /* scratch floats otamd_groupnorm_fwd / _bwd need for these sizes (partial slabs, coefficients, sums) */
 long long otamd_groupnorm_ws_floats(int N, int HW, int C);
 

@@ -94,6 +94,7 @@ SIGNATURES: dict[str, list] = {
     # norm.hip
     "otamd_groupnorm_fwd": [VP, LL, VP, LL, I, I, I, I, F, VP, VP, I, VP, VP, VP, VP, VP, VP],
     "otamd_groupnorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, I, I, VP, I, VP, VP, VP, VP, VP, VP, I, I, VP, I, VP],
+    "otamd_groupnorm_bwd_res": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, I, I, VP, I, VP, VP, VP, VP, VP, VP, I, I, VP, VP],
     "otamd_groupnorm_ws_floats": [I, I, I],
     "otamd_layernorm_fwd": [VP, LL, VP, LL, I, I, F, VP, VP, VP, VP, VP],
     "otamd_layernorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],

@@ -278,7 +278,8 @@ __global__ void __launch_bounds__(512) gn_bwd_apply_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ dx, long long lddx, int N, int HW, int C,
                                                            int pix_per_block, const float* __restrict__ a,
                                                            const float* __restrict__ b, const float* __restrict__ coef,
-                                                           int accumulate) {
+                                                           int accumulate, const bf16_t* __restrict__ res = nullptr,
+                                                           long long ldres = 0) {
   const int n = blockIdx.y;
   const int C8 = C >> 3;
   const int PPP = blockDim.x / C8;
@@ -295,18 +296,22 @@ __global__ void __launch_bounds__(512) gn_bwd_apply_kernel(const bf16_t* __restr
   const bf16_t* xb = x + (long long)n * HW * ldx + c8 * 8;
   const bf16_t* gb = dy + (long long)n * HW * lddy + c8 * 8;
   bf16_t* ob = dx + (long long)n * HW * lddx + c8 * 8;
+  const bf16_t* rb = res ? res + (long long)n * HW * ldres + c8 * 8 : nullptr;
   auto body = [&](int pp, const bf8& xv, const bf8& gv) {
     float xf[8], gf[8], o[8];
     unpack8(xv, xf);
     unpack8(gv, gf);
     float prev[8];
     if (accumulate) unpack8(*reinterpret_cast<const bf8*>(ob + (long long)pp * lddx), prev);
+    float rv[8];
+    if (res) unpack8(*reinterpret_cast<const bf8*>(rb + (long long)pp * ldres), rv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float dz = gf[j];
       if (SILU) dz *= dsilu_f(fmaf(xf[j], av[j], bv[j]));
       o[j] = fmaf(A[j], dz, fmaf(Bv[j], xf[j], Cc[j]));
       if (accumulate) o[j] += prev[j];
+      if (res) o[j] += rv[j];
     }
     *reinterpret_cast<bf8*>(ob + (long long)pp * lddx) = pack8(o);
   };
@@ -368,15 +373,17 @@ OTAMD_API int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long lo
   return OTAMD_OK;
 }
 
-// ws: otamd_groupnorm_ws_floats floats (8-byte aligned)
-OTAMD_API int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx,
-                                  long long lddx, int N, int HW, int C, int G, const void* gamma, int silu,
-                                  const float* mean, const float* rstd, const float* a, const float* b,
-                                  void* dgamma, void* dbeta, int param_f32, int param_acc, float* ws,
-                                  int accumulate, hipStream_t stream) {
+// res (nullable): dx += res in the apply pass -- the input's gradient through its other (residual /
+// shortcut) use, summed here instead of by a separate autograd add
+static int groupnorm_bwd_impl(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long lddx,
+                              int N, int HW, int C, int G, const void* gamma, int silu, const float* mean,
+                              const float* rstd, const float* a, const float* b, void* dgamma, void* dbeta,
+                              int param_f32, int param_acc, float* ws, int accumulate, const void* res,
+                              long long ldres, hipStream_t stream) {
   if (!x || !dy || !dx || !mean || !rstd || !a || !b || !ws || N <= 0 || HW <= 0) return OTAMD_EINVAL;
   if (C % 8 || C % G || ldx % 8 || lddy % 8 || lddx % 8 || C > 8192 || ((uintptr_t)ws & 7)) return OTAMD_EINVAL;
   if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) return OTAMD_EINVAL;
+  if (res && (ldres % 8 || ((uintptr_t)res & 15) || accumulate)) return OTAMD_EINVAL;
   const int C8 = C / 8, nt = gn_threads(C8);
   if (nt > 512) return OTAMD_EINVAL;
   const int ppb = gn_pix_per_block(N, HW, C8);
@@ -402,12 +409,36 @@ OTAMD_API int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, 
   }
   if (silu)
     gn_bwd_apply_kernel<true><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, (bf16_t*)dx,
-                                                        lddx, N, HW, C, ppb, a, b, coef, accumulate);
+                                                        lddx, N, HW, C, ppb, a, b, coef, accumulate,
+                                                        (const bf16_t*)res, ldres);
   else
     gn_bwd_apply_kernel<false><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, (bf16_t*)dx,
-                                                         lddx, N, HW, C, ppb, a, b, coef, accumulate);
+                                                         lddx, N, HW, C, ppb, a, b, coef, accumulate,
+                                                         (const bf16_t*)res, ldres);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
+}
+
+// ws: otamd_groupnorm_ws_floats floats (8-byte aligned)
+OTAMD_API int otamd_groupnorm_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx,
+                                  long long lddx, int N, int HW, int C, int G, const void* gamma, int silu,
+                                  const float* mean, const float* rstd, const float* a, const float* b,
+                                  void* dgamma, void* dbeta, int param_f32, int param_acc, float* ws,
+                                  int accumulate, hipStream_t stream) {
+  return groupnorm_bwd_impl(x, ldx, dy, lddy, dx, lddx, N, HW, C, G, gamma, silu, mean, rstd, a, b, dgamma, dbeta,
+                            param_f32, param_acc, ws, accumulate, nullptr, 0, stream);
+}
+
+// dx = GroupNorm(+SiLU)-backward(dy) + dres in the apply pass (dres: the gradient of the GroupNorm input through
+// its residual / shortcut use: ResnetBlock2D norm1 + shortcut, Transformer2DModel norm + proj_out residual)
+OTAMD_API int otamd_groupnorm_bwd_res(const void* x, long long ldx, const void* dy, long long lddy, const void* dres,
+                                      long long ldres, void* dx, long long lddx, int N, int HW, int C, int G,
+                                      const void* gamma, int silu, const float* mean, const float* rstd, const float* a,
+                                      const float* b, void* dgamma, void* dbeta, int param_f32, int param_acc,
+                                      float* ws, hipStream_t stream) {
+  if (!dres) return OTAMD_EINVAL;
+  return groupnorm_bwd_impl(x, ldx, dy, lddy, dx, lddx, N, HW, C, G, gamma, silu, mean, rstd, a, b, dgamma, dbeta,
+                            param_f32, param_acc, ws, 0, dres, ldres, stream);
 }
 
 // ------------------------------------------------------------------------------------------

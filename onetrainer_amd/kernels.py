@@ -540,8 +540,9 @@ def groupnorm_fwd(x, gamma, beta, groups, eps, silu, out=None):
 
 
 def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, need_param_grads=True,
-                  dgamma=None, dbeta=None, param_acc=False):
-    """returns (dx, dgamma, dbeta); pass dgamma/dbeta (bf16 or f32 grad views) to write them in place."""
+                  dgamma=None, dbeta=None, param_acc=False, dres=None):
+    """returns (dx, dgamma, dbeta); pass dgamma/dbeta (bf16 or f32 grad views) to write them in place.
+    dres: the input's gradient through its residual / shortcut use, added in the apply pass (dx = GN'(dy) + dres)."""
     N = x.shape[0]
     _, C_, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
@@ -556,6 +557,15 @@ def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, 
         dbeta = torch.empty(C_, dtype=F32, device=dev)
     pf32 = int(dgamma is not None and dgamma.dtype == F32)
     ws = workspace(4 * lib().otamd_groupnorm_ws_floats(N, HW, C_), dev)
+    if dres is not None:
+        _req(dres.shape == x.shape and dres.dtype == BF16 and _aligned(dres) and not accumulate,
+             "groupnorm residual grad: bf16, shape of x, 16-byte aligned")
+        _, _, ldres = _rows2d(dres)
+        check(lib().otamd_groupnorm_bwd_res(_p(x), ldx, _p(dy), lddy, _p(dres), ldres, _p(dx), lddx, N, HW, C_, groups,
+                                            _p(gamma), int(silu), _p(mean), _p(rstd), _p(a), _p(b), _p(dgamma),
+                                            _p(dbeta), pf32, int(param_acc), _p(ws), stream_handle()),
+              "otamd_groupnorm_bwd_res")
+        return dx, dgamma, dbeta
     check(lib().otamd_groupnorm_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, N, HW, C_, groups, _p(gamma), int(silu),
                                     _p(mean), _p(rstd), _p(a), _p(b), _p(dgamma), _p(dbeta), pf32, int(param_acc),
                                     _p(ws), int(accumulate), stream_handle()), "otamd_groupnorm_bwd")

@@ -339,6 +339,41 @@ def group_norm(x, gref, bref, groups, eps, silu):
     return GroupNormFn.apply(x, gref, bref, groups, eps, silu, *_params(gref, bref))
 
 
+class GroupNormResFn(torch.autograd.Function):
+    """(GroupNorm(+SiLU)(x), x) for a GroupNorm whose input also feeds a residual / shortcut (diffusers
+    ResnetBlock2D: norm1 and the identity or conv_shortcut path; Transformer2DModel: norm and the proj_out
+    residual).  The second output aliases x; backward receives both gradient contributions and sums them in
+    the GroupNorm-backward apply pass (otamd_groupnorm_bwd_res) instead of leaving an autograd add kernel."""
+
+    @staticmethod
+    def forward(ctx, x, gref, bref, groups, eps, silu, *params):
+        y, stats = K.groupnorm_fwd(x, gref.w, bref.w, groups, eps, silu)
+        ctx.save_for_backward(x, *stats)
+        ctx.gref, ctx.bref, ctx.groups, ctx.silu = gref, bref, groups, silu
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        x, *stats = ctx.saved_tensors
+        tr = ctx.gref.trainable
+        if dres is not None and (dres.stride(-1) != 1 or not dres.is_contiguous() or dres.data_ptr() % 16):
+            dres = dres.contiguous()
+        if dy is None:   # only the residual use reached backward
+            dy = torch.zeros_like(x)
+        dx, _, _ = K.groupnorm_bwd(x, dy, ctx.gref.w, ctx.groups, ctx.silu, stats,
+                                   dgamma=ctx.gref.g if tr else None, dbeta=ctx.bref.g if tr else None,
+                                   param_acc=tr and ctx.gref.acc(), need_param_grads=tr, dres=dres)
+        if tr:
+            ctx.gref.done()
+            ctx.bref.done()
+        return (dx if ctx.needs_input_grad[0] else None,) + (None,) * (len(ctx.needs_input_grad) - 1)
+
+
+def group_norm_res(x, gref, bref, groups, eps, silu):
+    """-> (GroupNorm(+SiLU)(x), residual alias of x); see GroupNormResFn."""
+    return GroupNormResFn.apply(x, gref, bref, groups, eps, silu, *_params(gref, bref))
+
+
 class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gref, bref, eps, *params):

@@ -331,9 +331,15 @@ class UNet2DConditionModel:
         return Fn.group_norm(x, self.R(p + ".weight"), self.R(p + ".bias"), cfg.norm_num_groups,
                              cfg.norm_eps if eps is None else eps, silu)
 
+    def _gn_res(self, x, p, silu, eps=None):
+        """(GroupNorm(x), alias of x for its residual / shortcut use): the two gradients of x meet in the
+        GroupNorm backward (Fn.GroupNormResFn), not in an autograd add."""
+        cfg = self.cfg
+        return Fn.group_norm_res(x, self.R(p + ".weight"), self.R(p + ".bias"), cfg.norm_num_groups,
+                                 cfg.norm_eps if eps is None else eps, silu)
+
     def _resnet(self, x, p, semb):
-        cin = x.shape[-1]
-        h = self._gn(x, p + ".norm1", True)
+        h, x = self._gn_res(x, p + ".norm1", True)
         tp = self._linear(semb, p + ".time_emb_proj")
         h = self._conv(h, p + ".conv1", rowvec=tp)
         h = self._gn(h, p + ".norm2", True)
@@ -394,7 +400,7 @@ class UNet2DConditionModel:
     def _transformer(self, x, p, depth, ehs):
         B, H, W, C = x.shape
         heads = self.cfg.heads(C)
-        h = self._gn(x, p + ".norm", False, eps=1e-6)
+        h, x = self._gn_res(x, p + ".norm", False, eps=1e-6)
         h = self._linear(h.view(B, H * W, C), p + ".proj_in")
         kv_all = self._kv_batched(p, depth, C, ehs)
         for k in range(depth):

@@ -38,9 +38,16 @@ def test_groupnorm(dev, N, H, W, C, G, silu, eps):
     assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 2e-2
     assert rel_err(dg, gr.grad) < 1e-2
     assert rel_err(db, br.grad) < 1e-2
+    # the input's residual-use gradient added in the apply pass (ResnetBlock2D shortcut): the same dx + dres,
+    # rounded once (vs the separate pass + bf16 add: within one bf16 rounding of each other)
+    dres = rnd(N, H, W, C, dev=dev, scale=0.7)
+    dx2, _, _ = K.groupnorm_bwd(x, dy, gamma, G, silu, stats, dres=dres)
+    ref2 = xr.grad.permute(0, 2, 3, 1) + dres.float()
+    assert rel_err(dx2, ref2) < 2e-2
+    assert (dx2.float() - (dx.float() + dres.float())).abs().max().item() <= 2 ** -7 * ref2.abs().max().item()
 
 
-@pytest.mark.parametrize("rows,C", [(4096, 640), (1000, 1280), (77, 320), (16384, 640), (4096, 1280), (31, 1280),
+@pytest.mark.parametrize("rows,C", [(4096, 640),(1000, 1280), (77, 320), (16384, 640), (4096, 1280), (31, 1280),
                                     (2381, 1536)])
 def test_layernorm(dev, rows, C):
     torch.manual_seed(1)

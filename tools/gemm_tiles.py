@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--top", type=int, default=14)
     ap.add_argument("--lora", type=int, default=0)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tiles", default="0,1,2,4,7,8", help="candidate tile codes (otamd_gemm_explicit)")
+    ap.add_argument("--skip", type=int, default=0, help="skip the first N signatures (by step time)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = TrainConfig.default_values()
@@ -68,7 +70,8 @@ def main():
         rows.append((sum(e0.elapsed_time(e1) for e0, e1 in evs), key, a, n))
     rows.sort(key=lambda r: -r[0])
     lib = _lib.lib()
-    for tot, key, a0, n in rows[:args.top]:
+    tiles = tuple(int(t) for t in args.tiles.split(","))
+    for tot, key, a0, n in rows[args.skip:args.skip + args.top]:
         a = K.GemmArgs.from_buffer_copy(a0)
         a.accumulate = 0
         esz = 4 if a.c_f32 else 2
@@ -86,7 +89,7 @@ def main():
                 continue
             ws_bytes = se * a.M * a.N * 4 if se > 1 else 0
             ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
-            for t in (0, 1, 2, 4, 7, 8):
+            for t in tiles:
                 rc = lib.otamd_gemm_explicit(C.byref(a), t, se, ws.data_ptr(), ws_bytes, K.stream_handle())
                 if rc != 0:
                     continue
