@@ -135,14 +135,19 @@ def gemm_roofline(tr, batch, in_step: bool = True):
     return flops, ms, len(recs)
 
 
-def pmc_traffic():
-    """GEMM-family memory-side traffic per step from the committed PMC passes (tools/gpu_pmc.sh:
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs, FETCH_SIZE doubled for gfx950)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic_sdxl1024_b4.json")
+TRAFFIC_FILES = {"sdxl": "pmc_traffic_sdxl1024_b4.json", "sd15": "pmc_traffic_sd15.json",
+                 "sdxl-lora": "pmc_traffic_sdxl-lora.json", "flux": "pmc_traffic_flux.json"}
+
+
+def pmc_traffic(model: str):
+    """GEMM-family memory-side traffic per step of this config from its committed PMC passes
+    (tools/gpu_counters.sh -> tools/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs of
+    this bench at its default shape, FETCH_SIZE doubled for gfx950).  (path, data) or (path, None)."""
+    path = os.path.join(ROOT, "profiles", TRAFFIC_FILES[model])
     if not os.path.exists(path):
-        return None
+        return path, None
     with open(path) as f:
-        return json.load(f)
+        return path, json.load(f)
 
 
 def launch_ranks(n: int) -> int:
@@ -300,7 +305,9 @@ def main():
         vae = vae_run(args.res, args.batch, iters=5, warmup=1, device=str(dev))
     g_achieved = g_flops / (g_ms * 1e-3) / 1e12
     i_achieved = i_flops / (i_ms * 1e-3) / 1e12
-    pmc = pmc_traffic()
+    pmc_path, pmc = pmc_traffic(args.model)
+    default_shape = (args.batch, args.res) == {"sdxl": (4, 1024), "sd15": (16, 512), "sdxl-lora": (4, 1024),
+                                               "flux": (4, 768)}[args.model]
 
     imgs = args.batch * world * args.steps
     value = imgs / elapsed
@@ -360,9 +367,10 @@ def main():
         "loss": round(loss_val, 5),
         "roofline": {"bound": "mfma", "achieved": round(g_achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(g_achieved / PEAK_BF16_TFLOPS, 4),
-                     "traffic": (pmc["gemm_total_gb"] if pmc and not (sd15 or flux or sdxl_lora) else None),
+                     "traffic": (pmc["gemm_total_gb"] if pmc and default_shape else None),
                      "traffic_unit": "GB per step, GEMM family (FETCH_SIZE x 2 + WRITE_SIZE, memory-side L2 counters: "
-                                     "Infinity-Cache hits included), from profiles/pmc_traffic_sdxl1024_b4.json",
+                                     f"Infinity-Cache hits included), from profiles/{os.path.basename(pmc_path)} "
+                                     "(PMC passes of this config's bench at its default shape)",
                      "algorithmic_gb": round(gemm_roofline.algo_bytes / 1e9, 2),
                      "kernel": "bf16 MFMA GEMM / implicit-GEMM conv (gemm2_kernel<*>, gemm_kernel, splitk_reduce_kernel)",
                      "basis": f"sum(2*M*N*K) over the {g_n} GEMM/conv launches of one step / sum of their in-step "

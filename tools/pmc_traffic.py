@@ -3,7 +3,7 @@
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of a wide
 (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.  Both are
 memory-side L2 counters, so Infinity-Cache hits are included (an upper bound on HBM bytes).
-One step = the dispatches after the second-to-last fused-AdamW launch up to and including the
+One step = the dispatches after the second-to-last fused-AdamW (bf16 or f32) launch up to and including the
 last one (bench.py's last timed step; the roofline's extra eager GEMM step comes after it and is
 excluded by taking the step that ends at the second-to-last AdamW when three or more exist).
 
@@ -43,7 +43,7 @@ def family(name):
 
 def step_window(rows):
     ids = sorted(rows)
-    marks = [i for i in ids if "adamw_bf16" in rows[i][0]]
+    marks = [i for i in ids if "adamw_" in rows[i][0]]   # bf16 (full fine-tune) or f32 (LoRA) update
     if len(marks) >= 3:
         lo, hi = marks[-3], marks[-2]
     else:
@@ -65,7 +65,7 @@ def main():
             launches[k] = launches.get(k, 0) + 1
         out[label] = {k: round(v / 1e9, 3) for k, v in fam.items()}
         out[label + "_launches"] = launches
-    out["unit"] = "GB per train step (SDXL 1024^2 b=4), FETCH_SIZE x 2 + WRITE_SIZE"
+    out["unit"] = "GB per train step of the profiled bench config, FETCH_SIZE x 2 + WRITE_SIZE"
     g = out["read"].get("gemm", 0.0) + out["write"].get("gemm", 0.0)
     out["gemm_total_gb"] = round(g, 3)
     out["gemm_launches"] = out["read_launches"].get("gemm", 0)
