@@ -3,8 +3,9 @@
     python -m onetrainer_amd.build            # incremental
     python -m onetrainer_amd.build --force
 
-Output: onetrainer_amd/_lib/libotamd.so (git-ignored; travels to the GPU box with the
-snapshot).  Every exported symbol is declared in include/otamd.h.
+Output: onetrainer_amd/_lib/libotamd.so and the native host layer _lib/_otamd_host.so (git-ignored;
+travel to the GPU box with the snapshot).  Every exported symbol of libotamd.so is declared in
+include/otamd.h.
 """
 from __future__ import annotations
 
@@ -54,6 +55,39 @@ def _compile(src: Path, force: bool) -> Path:
     return obj
 
 
+HOST_SRC = CSRC / "host" / "ops_host.cpp"
+HOST_LIB = LIB_DIR / "_otamd_host.so"
+INCLUDE = PKG.parent / "include"
+
+
+def build_host(force: bool = False) -> Path:
+    """The native host layer (csrc/host/ops_host.cpp -> _lib/_otamd_host.so): a CPython extension over torch's
+    C++ tensor API that calls libotamd.so's C ABI (rpath $ORIGIN).  Host code only: plain g++."""
+    import sysconfig
+
+    import torch
+    import torch.utils.cpp_extension as ce
+    deps = [HOST_SRC, INCLUDE / "otamd.h", LIB]
+    if not force and HOST_LIB.exists() and HOST_LIB.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
+        return HOST_LIB
+    cxx = shutil.which("g++") or "c++"
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", str(HOST_SRC),
+           "-o", str(HOST_LIB.with_suffix(".so.tmp")), f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           "-DTORCH_EXTENSION_NAME=_otamd_host", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           "-I", str(INCLUDE), "-I", "/opt/rocm/include", "-I", sysconfig.get_paths()["include"]]
+    for d in ce.include_paths():
+        cmd += ["-isystem", d]
+    for d in ce.library_paths():
+        cmd += ["-L", d, f"-Wl,-rpath,{d}"]
+    cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-L", str(LIB_DIR), "-lotamd", "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host layer build failed:\n{r.stderr[-6000:]}")
+    os.replace(HOST_LIB.with_suffix(".so.tmp"), HOST_LIB)
+    return HOST_LIB
+
+
 def build(force: bool = False, jobs: int | None = None) -> Path:
     OBJ.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
@@ -68,6 +102,7 @@ def build(force: bool = False, jobs: int | None = None) -> Path:
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
         os.replace(tmp, LIB)
+    build_host(force)
     return LIB
 
 

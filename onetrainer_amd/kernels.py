@@ -230,6 +230,56 @@ def _gemm(a: GemmArgs, splits: int, device) -> None:
     check(lib().otamd_gemm(C.byref(a), s_out.value, _p(ws), ws_bytes, stream_handle()), "otamd_gemm")
 
 
+# ---- native host layer ----------------------------------------------------------------------
+# csrc/host/ops_host.cpp (_lib/_otamd_host.so, built by build.py next to libotamd.so): the same functions as
+# below, one C++ call per op (shape checks on tensor metadata, at::empty outputs, the plan table in an
+# unordered_map, split-K workspaces per stream).  The Python paths below stay for the autotuner / plan
+# overrides / forced split-K (tools) and as the A/B reference (OTAMD_HOST=0).
+_HOST = {"mod": None, "tried": False, "off": False}
+
+
+def _host():
+    if not _HOST["tried"]:
+        _HOST["tried"] = True
+        path = _lib.LIB_PATH.with_name("_otamd_host.so")
+        if os.environ.get("OTAMD_HOST", "1") != "0" and path.exists() and not os.environ.get("OTAMD_LIB_ALT"):
+            import importlib.util
+            lib()   # libotamd.so first (RTLD_GLOBAL): the host layer links it
+            spec = importlib.util.spec_from_file_location("_otamd_host", str(path))
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            mod.set_plan_table([list(k) + [t, sp] for k, (t, sp) in _plan_table().items()])
+            import atexit
+            atexit.register(mod.clear_workspaces)   # free the cached workspaces while the allocator still exists
+            _HOST["mod"] = mod
+    if _HOST["off"] or _TUNE["on"] or _gemm_forced_splits or _plan_overrides_active():
+        return None
+    return _HOST["mod"]
+
+
+class python_host:
+    """context manager: launch through the ctypes path (A/B parity of the native host layer)."""
+
+    def __enter__(self):
+        self.prev, _HOST["off"] = _HOST["off"], True
+        return self
+
+    def __exit__(self, *exc):
+        _HOST["off"] = self.prev
+
+
+def _plan_overrides_active() -> bool:
+    global _PLAN_OVERRIDES
+    if _PLAN_OVERRIDES is None:
+        _PLAN_OVERRIDES = _plan_overrides()
+    return bool(_PLAN_OVERRIDES)
+
+
+def host_layer() -> str:
+    """which host path launches the ops: 'native' (C++ layer) or 'python' (ctypes)."""
+    return "native" if _host() is not None else "python"
+
+
 def _new_args() -> GemmArgs:
     a = GemmArgs()
     a.alpha = 1.0
@@ -299,6 +349,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, rowvec=No
            out=None, out_dtype=BF16, alpha=1.0, accumulate=False, lora=None) -> torch.Tensor:
     """y[M,N] = alpha * x[M,K] @ w[N,K]^T (+bias[N]) (+rowvec[m//rows_per_vec]) (+residual).
     lora = (t [M,r], b2 [N,r]): y += t @ b2^T, fused into the same GEMM as a second K segment."""
+    h = _host()
+    if h is not None:
+        lt, lb = lora if lora is not None else (None, None)
+        return h.linear(x, w, bias, residual, rowvec, rows_per_vec, out, out_dtype == F32, alpha, accumulate, lt, lb,
+                        stream_handle())
     _req(x.dtype == BF16 and w.dtype == BF16 and x.is_cuda, "linear: bf16 cuda tensors")
     M, K = x.shape
     N, K2 = w.shape
@@ -321,6 +376,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, rowvec=No
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, accumulate=False,
                  lora=None) -> torch.Tensor:
     """dx[M,K] = dy[M,N] @ w[N,K].  lora = (u [M,r], a2 [r,K]): dx += u @ a2 (second K segment)."""
+    h = _host()
+    if h is not None:
+        lu, la = lora if lora is not None else (None, None)
+        return h.linear_dgrad(dy, w, out, residual, accumulate, lu, la, stream_handle())
     _req(dy.dtype == BF16 and w.dtype == BF16, "linear_dgrad: bf16")
     M, N = dy.shape
     N2, K = w.shape
@@ -351,6 +410,10 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out=None, accumulate=False, 
     """dw[N,K] = alpha * dy[T,N]^T @ x[T,K]  (split-K over tokens T, deterministic slab reduce).
     bias_grad [N]: also db = sum_t dy[t, :] (unscaled; overwritten or, bias_acc, accumulated), from the dy
     image the GEMM already stages (no second pass over dy)."""
+    h = _host()
+    if h is not None:
+        return h.linear_wgrad(dy, x, out, accumulate, splits or 0, alpha, bias_grad, bias_acc,
+                              stream_handle())
     _req(dy.dtype == BF16 and x.dtype == BF16, "linear_wgrad: bf16")
     T, N = dy.shape
     T2, K = x.shape
@@ -396,6 +459,11 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias=None, stride=1, pad=1, upsampl
     upsample=True reads x through a nearest-2x upsample (diffusers Upsample2D).  out_hw overrides the
     output size: taps past the bottom / right edge read zeros, so pad=0 with out_hw = (H/2, W/2)
     is the VAE Downsample2D's F.pad(x, (0, 1, 0, 1)) + stride-2 conv."""
+    h = _host()
+    if h is not None:
+        lt, lb = lora if lora is not None else (None, None)
+        oh, ow = out_hw if out_hw is not None else (0, 0)
+        return h.conv2d(x, w, bias, stride, pad, upsample, residual, rowvec, out, lt, lb, oh, ow, stream_handle())
     N, H, W, Cin, ldx = _nhwc(x)
     Cout, KH, KW, Cin2 = w.shape
     _req(Cin2 == Cin and w.dtype == BF16 and w.is_contiguous() and Cout % 8 == 0, "conv weight [Cout,KH,KW,Cin]")
@@ -428,6 +496,9 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw, stride=1, pad=1, out=
                  accumulate=False) -> torch.Tensor:
     """dx of conv2d (no upsample): dx[n,h,w,ci] = sum_{r,s,co} dy[n,(h+pad-r)/st,(w+pad-s)/st,co] * w[co,r,s,ci].
     w is the stored weight [Cout][KH][KW][Cin], read in place (OPM_CONV_WT: no transpose pass)."""
+    h = _host()
+    if h is not None:
+        return h.conv2d_dgrad(dy, w, in_hw[0], in_hw[1], stride, pad, out, accumulate, stream_handle())
     N, P, Q, Cout, ldy = _nhwc(dy)
     Cout2, KH, KW, Cin = w.shape
     _req(Cout2 == Cout and w.is_contiguous() and Cin % 8 == 0 and Cout % 8 == 0 and _aligned(w),
@@ -451,6 +522,11 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ksize=3, stride=1, pad=1, up
                  accumulate=False, splits=None, bias_grad=None, bias_acc=False) -> torch.Tensor:
     """dw[co,r,s,ci] = sum_{n,p,q} dy[n,p,q,co] * x[n, p*st+r-pad, q*st+s-pad, ci]; bias_grad [Cout]: also
     db = sum_{n,p,q} dy[n,p,q,:] fused into the same GEMM."""
+    h = _host()
+    if h is not None:
+        return h.conv2d_wgrad(dy, x, ksize, stride, pad, upsample, out, accumulate, splits or 0, bias_grad,
+                              bias_acc,
+                              stream_handle())
     N, P, Q, Cout, ldy = _nhwc(dy)
     N2, H, W, Cin, ldx = _nhwc(x)
     _req(N == N2 and conv_out_hw(H, W, ksize, stride, pad, upsample) == (P, Q), "wgrad geometry")
@@ -521,6 +597,9 @@ def _rows2d(x: torch.Tensor):
 
 def groupnorm_fwd(x, gamma, beta, groups, eps, silu, out=None):
     """x: [N, H, W, C] (or [N, HW, C]) bf16 -> y = [silu](GroupNorm(x)); returns (y, stats)."""
+    h = _host()
+    if h is not None and out is None:
+        return h.groupnorm_fwd(x, gamma, beta, groups, eps, silu, stream_handle())
     N = x.shape[0]
     _, C_, ldx = _rows2d(x)
     HW = x.numel() // (N * C_)
@@ -543,6 +622,15 @@ def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, 
                   dgamma=None, dbeta=None, param_acc=False, dres=None):
     """returns (dx, dgamma, dbeta); pass dgamma/dbeta (bf16 or f32 grad views) to write them in place.
     dres: the input's gradient through its residual / shortcut use, added in the apply pass (dx = GN'(dy) + dres)."""
+    h = _host()
+    if h is not None and dx is None and not accumulate:
+        if dgamma is None and need_param_grads:
+            dgamma = torch.empty(x.shape[-1], dtype=F32, device=x.device)
+            dbeta = torch.empty(x.shape[-1], dtype=F32, device=x.device)
+        mean, rstd, a, b = stats
+        dx = h.groupnorm_bwd(x, dy, gamma, groups, silu, mean, rstd, a, b, dgamma, dbeta, param_acc, dres,
+                             stream_handle())
+        return dx, dgamma, dbeta
     N = x.shape[0]
     _, C_, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
@@ -573,6 +661,9 @@ def groupnorm_bwd(x, dy, gamma, groups, silu, stats, dx=None, accumulate=False, 
 
 
 def layernorm_fwd(x, gamma, beta, eps, out=None):
+    h = _host()
+    if h is not None and out is None:
+        return h.layernorm_fwd(x, gamma, beta, eps, stream_handle())
     rows, C_, ldx = _rows2d(x)
     if out is None:
         out = torch.empty(x.shape, dtype=BF16, device=x.device)
@@ -605,6 +696,11 @@ def layernorm_bwd(x, dy, gamma, stats, dx=None, accumulate=False, dgamma=None, d
 
 def layernorm_bwd_res(x, dy, dres, gamma, stats):
     """dx = LayerNorm-backward(dy) + dres (the input's gradient through its residual use), one pass."""
+    h = _host()
+    if h is not None:
+        dx = h.layernorm_bwd_res(x, dy, dres, gamma, stats[0], stats[1], stream_handle())
+        if dx is not None:
+            return dx
     rows, C_, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
     _req(dres.shape == x.shape and dres.dtype == BF16, "layernorm residual grad: bf16, shape of x")
@@ -623,6 +719,10 @@ def layernorm_bwd_res(x, dy, dres, gamma, stats):
 
 def layernorm_param_grad(x, dy, stats, dgamma, dbeta, param_acc=False):
     """dgamma += / = sum_rows dy * xhat, dbeta = sum_rows dy (bf16 or f32 destinations)."""
+    h = _host()
+    if h is not None:
+        h.layernorm_param_grad(x, dy, stats[0], stats[1], dgamma, dbeta, param_acc, stream_handle())
+        return dgamma, dbeta
     rows, C_, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
     _req(dgamma.dtype == dbeta.dtype and dgamma.dtype in (BF16, F32), "layernorm param grads bf16 / f32")
@@ -778,6 +878,9 @@ def attn_fwd(q, k, v, heads, scale=None, out=None):
     kernels' lse [B,H,Nq] (log2 domain) for head dims <= 128, else the materialized P."""
     if q.shape[-1] // heads > FLASH_MAX_D:
         return attn_mat_fwd(q, k, v, heads, scale, out)
+    h = _host()
+    if h is not None:
+        return h.attn_fwd(q, k, v, heads, -1.0 if scale is None else scale, out, stream_handle())
     a = _attn_args(q, k, v, heads, scale)
     if out is None:
         out = torch.empty(q.shape, dtype=BF16, device=q.device)
@@ -791,6 +894,9 @@ def attn_fwd(q, k, v, heads, scale=None, out=None):
 def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None):
     if q.shape[-1] // heads > FLASH_MAX_D:
         return attn_mat_bwd(q, k, v, lse, dout, heads, scale, dq, dk, dv)
+    h = _host()
+    if h is not None:
+        return h.attn_bwd(q, k, v, o, lse, dout, heads, -1.0 if scale is None else scale, dq, dk, dv, stream_handle())
     a = _attn_args(q, k, v, heads, scale)
     dq = torch.empty(q.shape, dtype=BF16, device=q.device) if dq is None else dq
     dk = torch.empty(k.shape, dtype=BF16, device=q.device) if dk is None else dk
@@ -816,6 +922,9 @@ def _dense(t):
 
 
 def geglu_fwd(h, out=None):
+    hm = _host()
+    if hm is not None and out is None:
+        return hm.geglu_fwd(h, stream_handle())
     rows, C2, ldh = _rows2d(h)
     F_ = C2 // 2
     if out is None:
@@ -826,6 +935,9 @@ def geglu_fwd(h, out=None):
 
 
 def geglu_bwd(h, dout, dh=None):
+    hm = _host()
+    if hm is not None and dh is None:
+        return hm.geglu_bwd(h, dout, stream_handle())
     rows, C2, ldh = _rows2d(h)
     _, _, lddo = _rows2d(dout)
     if dh is None:

@@ -4,6 +4,7 @@ import re
 from pathlib import Path
 
 import pytest
+import torch
 
 from onetrainer_amd import _lib
 
@@ -36,3 +37,22 @@ def test_no_fallback_when_library_missing(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.lib()
+
+
+def test_native_host_layer_loads():
+    """the C++ host layer (_lib/_otamd_host.so) loads over libotamd.so, agrees on the struct layouts and maps
+    a violated contract to ValueError, like the ctypes path (no compute: CPU tensors are rejected)."""
+    from onetrainer_amd import kernels as K
+    h = K._host()
+    assert h is not None, "native host layer missing: run onetrainer_amd.build"
+    assert h.gemm_args_size() == _lib.lib().otamd_gemm_args_size()
+    assert h.attn_args_size() == _lib.lib().otamd_attn_args_size()
+    assert h.plan_table_size() == len(K._plan_table())
+    x = torch.zeros(4, 8, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="bf16 cuda"):
+        h.linear(x, x, None, None, None, 0, None, False, 1.0, False, None, None, 0)
+    with pytest.raises(ValueError, match="NHWC"):
+        h.conv2d(x, x, None, 1, 1, False, None, None, None, None, None, 0, 0, 0)
+    with K.python_host():
+        assert K._host() is None
+    assert K.host_layer() == "native"
