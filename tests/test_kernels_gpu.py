@@ -89,7 +89,8 @@ def sdpa_ref(q, k, v, heads):
                                          (1, 1024, 1024, 4, 64), (1, 256, 256, 2, 128), (2, 200, 77, 4, 40),
                                          (2, 2048, 2048, 4, 64), (1, 333, 1000, 2, 128), (1, 128, 50, 2, 64),
                                          (1, 192, 64, 2, 64), (1, 256, 128, 2, 64), (1, 200, 190, 2, 128),
-                                         (1, 160, 3, 2, 64)])
+                                         (1, 160, 3, 2, 64), (2, 1024, 96, 20, 64), (1, 100, 77, 3, 64),
+                                         (1, 1024, 97, 2, 64)])
 def test_attention(dev, B, Nq, Nk, H, D):
     torch.manual_seed(2)
     q, k, v = rnd(B, Nq, H * D, dev=dev), rnd(B, Nk, H * D, dev=dev), rnd(B, Nk, H * D, dev=dev)
