@@ -123,7 +123,10 @@ def gemm_roofline(tr, batch, in_step: bool = True):
     graphs, tr.graphs = tr.graphs, None   # an eager step: every GEMM launched (and timed) from the host
     K._gemm = timed
     try:
-        tr.train_step(batch)
+        # through the ctypes host path, whose _gemm the timer wraps: the same kernels with the same plans as the
+        # native host layer (bit-identical, tests/test_host_layer_gpu.py), only the host side of the launch differs
+        with K.python_host():
+            tr.train_step(batch)
         torch.cuda.synchronize()
     finally:
         K._gemm = orig

@@ -1,0 +1,28 @@
+"""bench.py's contract (the driver parses its one JSON line): a short run of the default workload at a small
+resolution must print a well-formed line with the roofline and timing fields."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_json_line():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--res", "256",
+                        "--batch", "1", "--no-cpu-baseline", "--no-vae"], capture_output=True, text=True, timeout=280,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["n_gpus"] == 1 and d["steps"] == 2
+    rf = d["roofline"]
+    assert rf["achieved"] > 0 and 0 < rf["frac"] < 1 and rf["peak"] > 0 and rf["isolated_frac"] > 0
+    assert d["config"]["parallelism"] == "dp1"
