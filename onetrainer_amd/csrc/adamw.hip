@@ -395,6 +395,30 @@ OTAMD_API int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void
   return OTAMD_OK;
 }
 
+// the grad-norm pass split over the backward (util/optimizer/adamw_fused.OverlappedGradNorm): the per-tensor
+// squared norms of chunks [c_begin, c_end) accumulated into tensor_sq (zeroed by the caller once per step) as
+// soon as those tensors' gradients are final, on the weight-gradient stream beside the dgrad chain ...
+OTAMD_API int otamd_grad_sqnorm_chunks(const void* grads, int grad_dtype, const void* chunks, int c_begin, int c_end,
+                                       double* tensor_sq, hipStream_t stream) {
+  if (!grads || !chunks || !tensor_sq || c_begin < 0 || c_end < c_begin) return OTAMD_EINVAL;
+  if (c_end == c_begin) return OTAMD_OK;
+  const NormChunk* c = (const NormChunk*)chunks + c_begin;
+  if (grad_dtype == 0) grad_sqnorm_kernel<bf16_t><<<c_end - c_begin, 256, 0, stream>>>((const bf16_t*)grads, c, tensor_sq);
+  else grad_sqnorm_kernel<float><<<c_end - c_begin, 256, 0, stream>>>((const float*)grads, c, tensor_sq);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
+// ... and the clip coefficient from the accumulated per-tensor sums (clip_grad_norm_'s torch dtypes, as
+// otamd_grad_clip_coef)
+OTAMD_API int otamd_grad_clip_finalize(const double* tensor_sq, int n_tensors, float max_norm, int grad_dtype,
+                                       float* out, hipStream_t stream) {
+  if (!tensor_sq || !out || n_tensors < 1) return OTAMD_EINVAL;
+  clip_coef_kernel<<<1, 1024, 0, stream>>>(tensor_sq, n_tensors, max_norm, grad_dtype == 0, out);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
 // scale a flat grad store by the device clip coefficient (used when the optimizer is
 // not the fused AdamW, e.g. parity checks of clip_grad_norm_ alone)
 __global__ void scale_bf16_kernel(bf16_t* __restrict__ g, long long n8, const float* __restrict__ coef) {

@@ -83,6 +83,20 @@ class GenericTrainer(TimedActionMixin):
         from .step_graph import StepGraphs
         if StepGraphs.enabled_for(self):
             self.graphs = StepGraphs(self)
+        self._attach_norm_overlap()
+
+    def _attach_norm_overlap(self):
+        """single process, eager steps, clip on, the fused AdamW: clip_grad_norm_'s norm pass runs during backward
+        (util/optimizer/adamw_fused.OverlappedGradNorm); data parallel clips the all-reduced gradients instead."""
+        import os
+
+        from ..module import streams as S
+        from ..util.optimizer.adamw_fused import FusedAdamW, OverlappedGradNorm
+        opt = getattr(self.model, "optimizer", None)
+        if (isinstance(opt, FusedAdamW) and self.world == 1 and self.graphs is None and self.config.clip_grad_norm
+                and opt.store.grad.is_cuda and S.enabled() and os.environ.get("OTAMD_NORM_OVERLAP", "1") != "0"
+                and opt.norm_overlap is None):
+            opt.norm_overlap = OverlappedGradNorm(opt)
 
     def _load_weights(self):
         """base / VAE / LoRA weights and a backup to continue from (GenericTrainer.py:92-108 +
@@ -215,14 +229,19 @@ class GenericTrainer(TimedActionMixin):
         update = self._is_update_step(tp)
         if self.reducer is not None:   # GA micro-steps accumulate locally; the update step's backward reduces
             self.reducer.arm(update)
+        norm = getattr(model.optimizer, "norm_overlap", None)
         loss = self.graphs.forward_backward(batch) if self.graphs is not None else None
         if loss is None:   # eager (or the first sight of a shape before its capture: trainer/step_graph.py)
             out = setup.predict(model, batch, cfg, tp)
             loss = setup.calculate_loss(model, batch, out, cfg)
             loss = loss / cfg.gradient_accumulation_steps
             store.begin_backward()
+            if norm is not None:
+                norm.arm(update and cfg.clip_grad_norm is not None)
             loss.backward()
             store.finish_backward()
+            if norm is not None:
+                norm.finish()
         if update:
             if self.reducer is not None:
                 self.reducer.finish()

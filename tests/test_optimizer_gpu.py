@@ -147,3 +147,42 @@ def test_overlapped_chunked_adamw_matches_single_launch(dev, monkeypatch):
         runs.append((st.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone()))
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+def test_grad_norm_during_backward_matches_end_of_step(dev):
+    """clip_grad_norm_'s norm pass spread over the backward (OverlappedGradNorm, per-bucket sums on the
+    weight-gradient stream) gives the same clip coefficient, total norm and updated parameters as the
+    end-of-step pass over the whole gradient buffer."""
+    from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_sdxl_batch
+    from onetrainer_amd.module import unet as U
+    from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util import create
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+
+    def run(overlap):
+        cfg = TrainConfig.default_values()
+        cfg.batch_size = 2
+        cfg.learning_rate_warmup_steps = 0
+        cfg.clip_grad_norm = 0.05   # small enough that clipping is active
+        model = create.create_model(cfg, dev, seed=7, unet_config=U.tiny_sdxl_config())
+        tr = GenericTrainer(cfg, model=model)
+        tr.start()
+        opt = model.optimizer
+        assert opt.norm_overlap is not None
+        if not overlap:
+            opt.norm_overlap = None
+        batch = synthetic_sdxl_batch(2, 128, 128, dev, seed=3, te1_dim=48, te2_dim=48, pooled_dim=64)
+        clips = []
+        for _ in range(2):
+            tr.train_step(batch)
+            clips.append(opt.clip_out.clone())
+        torch.cuda.synchronize()
+        return clips, model.train_store.data.clone()
+
+    c1, p1 = run(True)
+    c2, p2 = run(False)
+    for a, b in zip(c1, c2):
+        assert a[0].item() < 1.0                      # clipping active
+        assert a[0].item() == b[0].item()             # coefficient (bf16 value) identical
+        assert abs(a[1].item() - b[1].item()) <= 1e-6 * abs(b[1].item())
+    assert torch.equal(p1, p2)
