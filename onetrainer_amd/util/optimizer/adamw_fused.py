@@ -276,7 +276,6 @@ class OverlappedGradNorm:
             self.opt._tensor_sq.zero_()
 
     def _launch(self, bi, side):
-        from ...module import streams as S
         self.launched[bi] = True
         c0, c1, _ = self.buckets[bi]
         opt = self.opt
@@ -293,7 +292,6 @@ class OverlappedGradNorm:
             _lib.check(_lib.lib().otamd_grad_sqnorm_chunks(g.data_ptr(), dtype, opt._chunks.data_ptr(), c0, c1,
                                                            opt._tensor_sq.data_ptr(), K.stream_handle()),
                        "otamd_grad_sqnorm_chunks")
-        del S
 
     def _on_ready(self, names):
         if not self.armed:
