@@ -299,6 +299,14 @@ int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s)
 
 /* replaces: ModelSetupNoiseMixin._create_noise (modules/modelSetup/mixin/ModelSetupNoiseMixin.py:18-49) */
 int otamd_noise(void* out, int f32, long long n, long long offset, unsigned long long seed, hipStream_t s);
+/* replaces: the same with offset_noise_weight / perturbation_noise_weight > 0 (ModelSetupNoiseMixin.py:31-46):
+   noise + ow * N[sample, channel] (constant over the pixels), then + pw * N, each op rounded to the output
+   dtype in the reference's order.  NHWC tensor, hwc = h * w * C; offset = global element index of out[0]. */
+int otamd_noise_ex(void* out, int f32, long long n, long long offset, unsigned long long seed, int C,
+    long long hwc, float offset_weight, float perturbation_weight, hipStream_t s);
+/* test hook: raw standard-normal draws of Philox stream `stream_id` (1 = noise, 4 = offset, 5 = perturbation) */
+int otamd_noise_stream(void* out, int f32, long long n, long long offset, unsigned long long seed, int stream_id,
+    hipStream_t s);
 
 /* replaces: ModelSetupNoiseMixin._get_timestep_discrete (ModelSetupNoiseMixin.py:51-155), UNIFORM (dist 0) and
    LOGIT_NORMAL (dist 1) with static shift.  min_t / max_t = int(num_train_timesteps * min/max_noising_strength)

@@ -145,6 +145,8 @@ SIGNATURES: dict[str, list] = {
     "otamd_flux_pack": [VP, VP, I, I, I, I, I, I, VP],
     # diffusion.hip
     "otamd_noise": [VP, I, LL, LL, U64, VP],
+    "otamd_noise_ex": [VP, I, LL, LL, U64, I, LL, F, F, VP],
+    "otamd_noise_stream": [VP, I, LL, LL, U64, I, VP],
     "otamd_timesteps": [VP, I, LL, U64, I, I, I, I, F, F, F, VP, VP],
     "otamd_ddpm_prologue": [VP, VP, I, VP, VP, VP, VP, F, I, LL, I, I, VP, VP, I, VP, VP],
     "otamd_flow_prologue": [VP, VP, I, VP, F, F, I, I, LL, I, I, VP, VP, VP],

@@ -64,6 +64,35 @@ __global__ void noise_kernel(void* out, int f32, long long n, long long offset, 
     st_t(out, i, f32, round_t(philox_normal(seed, 1u, (uint64_t)(offset + i)), f32));
 }
 
+// noise with the reference's optional terms (ModelSetupNoiseMixin.py:24-46), one pass:
+//   noise = N_1 ; noise = noise + ow * N_4[sample, c] (offset noise, constant over the pixels) ;
+//   noise = noise + pw * N_5 (perturbation noise), each op rounded to the tensor dtype in the reference's
+//   order (python-float x tensor, then tensor + tensor).  NHWC [.., hw, C] layout: element g of the global
+//   tensor is sample g / hwc, channel g % C.  Stream 4 is indexed by sample * C + c, stream 5 like stream 1.
+__global__ void noise_ex_kernel(void* out, int f32, long long n, long long offset, unsigned long long seed, int C,
+                                long long hwc, float ow, float pw) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long g = offset + i;
+    float v = round_t(philox_normal(seed, 1u, (uint64_t)g), f32);
+    if (ow > 0.f) {
+      const float o = round_t(philox_normal(seed, 4u, (uint64_t)((g / hwc) * C + g % C)), f32);
+      v = round_t(v + round_t(ow * o, f32), f32);
+    }
+    if (pw > 0.f) {
+      const float q = round_t(philox_normal(seed, 5u, (uint64_t)g), f32);
+      v = round_t(v + round_t(pw * q, f32), f32);
+    }
+    st_t(out, i, f32, v);
+  }
+}
+
+// raw draws of one Philox normal stream (tests compose the reference's noise terms from them)
+__global__ void noise_stream_kernel(void* out, int f32, long long n, long long offset, unsigned long long seed,
+                                    unsigned stream) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    st_t(out, i, f32, round_t(philox_normal(seed, stream, (uint64_t)(offset + i)), f32));
+}
+
 // timesteps for samples [sample0, sample0+n) of the global batch
 // dist 0 = UNIFORM, 1 = LOGIT_NORMAL (ModelSetupNoiseMixin.py:91-118).  draws != nullptr injects the
 // random draw of each sample instead of Philox (parity tests): UNIFORM -> the U[0,1) sample of
@@ -247,6 +276,26 @@ OTAMD_API int otamd_noise(void* out, int f32, long long n, long long offset, uns
   if (!out || n < 0 || offset < 0) return OTAMD_EINVAL;
   if (n == 0) return OTAMD_OK;
   noise_kernel<<<gfor(n), 256, 0, s>>>(out, f32, n, offset, seed);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+// out: [n] elements of the global NHWC noise tensor starting at element `offset` (a whole number of samples
+// when ow > 0 is not required: the sample / channel come from the global element index); hwc = h * w * C
+OTAMD_API int otamd_noise_ex(void* out, int f32, long long n, long long offset, unsigned long long seed, int C,
+                             long long hwc, float offset_weight, float perturbation_weight, hipStream_t s) {
+  if (!out || n < 0 || offset < 0 || C <= 0 || hwc <= 0 || hwc % C || !(offset_weight >= 0.f) ||
+      !(perturbation_weight >= 0.f))
+    return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  noise_ex_kernel<<<gfor(n), 256, 0, s>>>(out, f32, n, offset, seed, C, hwc, offset_weight, perturbation_weight);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+OTAMD_API int otamd_noise_stream(void* out, int f32, long long n, long long offset, unsigned long long seed,
+                                 int stream_id, hipStream_t s) {
+  if (!out || n < 0 || offset < 0 || stream_id < 1) return OTAMD_EINVAL;
+  if (n == 0) return OTAMD_OK;
+  noise_stream_kernel<<<gfor(n), 256, 0, s>>>(out, f32, n, offset, seed, (unsigned)stream_id);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

@@ -1065,6 +1065,28 @@ def noise(shape, seed, offset=0, dtype=BF16, device=None, out=None):
     return out
 
 
+def noise_ex(shape, seed, offset=0, offset_weight=0.0, perturbation_weight=0.0, dtype=BF16, device=None, out=None):
+    """NHWC noise [B, h, w, C] with the reference's offset / perturbation terms (ModelSetupNoiseMixin.py:24-46);
+    equals noise() when both weights are 0."""
+    if out is None:
+        out = torch.empty(shape, dtype=dtype, device=device)
+    _req(tuple(out.shape) == tuple(shape) and out.dtype == dtype and out.is_contiguous() and len(shape) >= 2,
+         "noise_ex out")
+    C = int(shape[-1])
+    check(lib().otamd_noise_ex(_p(out), int(dtype == F32), out.numel(), offset, seed & 0xFFFFFFFFFFFFFFFF, C,
+                               out.numel() // max(1, int(shape[0])), float(offset_weight), float(perturbation_weight),
+                               stream_handle()), "otamd_noise_ex")
+    return out
+
+
+def noise_stream(n, seed, stream_id, offset=0, dtype=F32, device=None):
+    """raw draws [n] of one Philox normal stream (test hook)."""
+    out = torch.empty(n, dtype=dtype, device=device)
+    check(lib().otamd_noise_stream(_p(out), int(dtype == F32), n, offset, seed & 0xFFFFFFFFFFFFFFFF, stream_id,
+                                   stream_handle()), "otamd_noise_stream")
+    return out
+
+
 def timesteps(n, seed, sample0=0, dist=0, num_train_timesteps=1000, min_s=0.0, max_s=1.0, shift=1.0, bias=0.0,
               weight=0.0, device=None, out=None, draws=None):
     """draws: optional f32 [n] injected draws (U[0,1) for UNIFORM, the N(bias, weight+1) sample for LOGIT_NORMAL)."""

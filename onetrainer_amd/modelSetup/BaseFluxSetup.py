@@ -20,7 +20,7 @@ import torch
 from .. import kernels as K
 from ..module import flux_ops as O
 from ..module import functional as Fn
-from .BaseStableDiffusionXLSetup import loss_plan, nhwc_pair, timestep_plan
+from .BaseStableDiffusionXLSetup import draw_noise, loss_plan, nhwc_pair, report_learning_rates, timestep_plan
 from ..util.config.plain import plain
 
 
@@ -52,6 +52,9 @@ class BaseFluxSetup:
             ehs = ehs * m[:, None, None]
         return pooled.to(torch.bfloat16).contiguous(), ehs.to(torch.bfloat16).contiguous()
 
+    def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
+        report_learning_rates(model, lr_scheduler, tensorboard)
+
     def _shift(self, config, h, w):
         """ModelSetupNoiseMixin._get_timestep_discrete: static timestep_shift, or the dynamic one of the
         image sequence length (base 256 -> 0.5, max 4096 -> 1.15, patch 2)."""
@@ -64,8 +67,6 @@ class BaseFluxSetup:
 
     def predict(self, model, batch: dict, config, train_progress, *, deterministic: bool = False) -> dict:
         config = plain(config)
-        if config.offset_noise_weight > 0 or config.perturbation_noise_weight > 0:
-            raise NotImplementedError("offset / perturbation noise are not on this build's hot path yet")
         batch_seed = 0 if deterministic else train_progress.global_step
         rand = Random(batch_seed)
         latent = self._nhwc_latent(batch["latent_image"])
@@ -76,8 +77,7 @@ class BaseFluxSetup:
             noise, timestep = self.graph_inputs
         else:
             sample0 = self.dp_rank * B
-            noise = K.noise(latent.shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=latent.dtype,
-                            device=latent.device)
+            noise = draw_noise(config, latent.shape, batch_seed, sample0 * h * w * C, latent.dtype, latent.device)
             if deterministic:
                 timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=latent.device)
             else:

@@ -55,6 +55,31 @@ def timestep_plan(config) -> int:
     return TIMESTEP_DIST[d]
 
 
+def draw_noise(config, shape, seed, offset, dtype, device, out=None):
+    """_create_noise (ModelSetupNoiseMixin.py:18-49) for an NHWC latent: Philox stream 1, plus the offset
+    (per sample and channel) and perturbation terms when their weights are > 0, in one kernel."""
+    ow, pw = float(config.offset_noise_weight), float(config.perturbation_noise_weight)
+    if ow > 0 or pw > 0:
+        return K.noise_ex(shape, seed=seed, offset=offset, offset_weight=max(ow, 0.0), perturbation_weight=max(pw, 0.0),
+                          dtype=dtype, device=device, out=out)
+    return K.noise(shape, seed=seed, offset=offset, dtype=dtype, device=device, out=out)
+
+
+def report_learning_rates(model, lr_scheduler, tensorboard):
+    """BaseModelSetup.report_to_tensorboard (modules/modelSetup/BaseModelSetup.py:96-119): the scheduler's
+    last lr of each parameter group as `lr/<display name prefix>`, the first group of a prefix winning
+    (AdamW's maybe_adjust_lrs is the identity)."""
+    lrs = lr_scheduler.get_last_lr()
+    names = model.parameters.display_name_mapping()
+    if len(lrs) != len(names):
+        raise ValueError(f"{len(lrs)} learning rates for {len(names)} parameter groups")
+    reported = {}
+    for lr, name in zip(lrs, names):
+        reported.setdefault(name.split("/")[0], lr)
+    for name, lr in reported.items():
+        tensorboard.add_scalar(f"lr/{name}", lr, model.train_progress.global_step)
+
+
 def nhwc_pair(data: dict, C: int):
     """(pred NHWC bf16 [B,h,w,cpad], target NHWC [B,h,w,C]) for the loss kernel: the private kernel
     tensors predict() returned, or -- when a caller hands [B,C,h,w] tensors of its own -- their
@@ -105,13 +130,15 @@ class BaseStableDiffusionXLSetup:
                                                         te2.to(torch.bfloat16), pooled)
         return ehs, pooled
 
+    def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
+        report_learning_rates(model, lr_scheduler, tensorboard)
+
     def graphable(self, config) -> bool:
         """the step has no host-random or host-varying input besides (noise, timestep), so it can be
         captured once and replayed (text dropout draws its mask on the host per step)."""
         config = plain(config)
         parts = [config.text_encoder] + ([config.text_encoder_2] if hasattr(config, "text_encoder_2") else [])
-        return (config.offset_noise_weight <= 0 and config.perturbation_noise_weight <= 0
-                and all(not (p.dropout_probability or 0) > 0 for p in parts))
+        return all(not (p.dropout_probability or 0) > 0 for p in parts)
 
     def step_inputs(self, model, batch: dict, config, train_progress, *, deterministic: bool = False, out=None):
         """(noise, timestep) of this micro-step (ModelSetupNoiseMixin._create_noise /
@@ -123,8 +150,8 @@ class BaseStableDiffusionXLSetup:
         shape = tuple(self._nhwc_latent(lat).shape) if out is None else tuple(out[0].shape)
         _, h, w, C = shape
         sample0 = self.dp_rank * B                       # global-batch index of this rank's first sample
-        noise = K.noise(shape, seed=batch_seed, offset=sample0 * h * w * C, dtype=lat.dtype, device=lat.device,
-                        out=None if out is None else out[0])
+        noise = draw_noise(config, shape, batch_seed, sample0 * h * w * C, lat.dtype, lat.device,
+                           None if out is None else out[0])
         N = model.noise_scheduler.config["num_train_timesteps"]
         if deterministic:
             timestep = torch.full((B,), int(N * 0.5) - 1, dtype=torch.int32, device=lat.device)
@@ -140,8 +167,6 @@ class BaseStableDiffusionXLSetup:
 
     def predict(self, model, batch: dict, config, train_progress, *, deterministic: bool = False) -> dict:
         config = plain(config)
-        if config.offset_noise_weight > 0 or config.perturbation_noise_weight > 0:
-            raise NotImplementedError("offset / perturbation noise are not on this build's hot path yet")
         batch_seed = 0 if deterministic else train_progress.global_step
         rand = Random(batch_seed)
         latent = self._nhwc_latent(batch["latent_image"])

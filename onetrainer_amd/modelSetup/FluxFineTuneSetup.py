@@ -51,7 +51,3 @@ class FluxFineTuneSetup(BaseFluxSetup):
     def after_optimizer_step(self, model, config, train_progress):
         config = plain(config)
         pass
-
-    def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
-        config = plain(config)
-        pass

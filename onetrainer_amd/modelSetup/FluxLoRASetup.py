@@ -77,7 +77,3 @@ class FluxLoRASetup(BaseFluxSetup):
     def after_optimizer_step(self, model, config, train_progress):
         config = plain(config)
         model.transformer_lora.refresh()
-
-    def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
-        config = plain(config)
-        pass

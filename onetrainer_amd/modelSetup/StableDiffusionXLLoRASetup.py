@@ -75,7 +75,3 @@ class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
     def after_optimizer_step(self, model, config, train_progress):
         config = plain(config)
         model.unet_lora.refresh()
-
-    def report_to_tensorboard(self, model, config, lr_scheduler, tensorboard):
-        config = plain(config)
-        pass

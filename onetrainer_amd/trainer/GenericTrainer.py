@@ -44,6 +44,11 @@ class GenericTrainer(TimedActionMixin):
         self.reducer = None
         self.graphs = None
         self.loss_history: list[torch.Tensor] = []
+        self.tensorboard = None            # util/tensorboard.ScalarLog, opened by train()
+        self._micro_losses: list[torch.Tensor] = []         # this update step's micro-step losses (device)
+        self._update_losses: list[tuple[int, list[torch.Tensor]]] = []   # (global_step, losses) not yet logged
+        self._ema_loss = None
+        self._ema_loss_steps = 0
         self.one_step_trained = False
         self._has_gradient = False
         self._wallclock_timers = False
@@ -297,6 +302,8 @@ class GenericTrainer(TimedActionMixin):
         steps = 0
         frozen = False
         failed = True
+        if self.tensorboard is None:
+            self.tensorboard = self._open_scalar_log()
         try:
             for _epoch in range(tp.epoch, cfg.epochs):
                 self.data_loader.get_data_set().start_next_epoch()
@@ -313,8 +320,14 @@ class GenericTrainer(TimedActionMixin):
                             self.backup(tp)
                         if flags & 2:
                             self.save(tp)
+                    gs, update = tp.global_step, self._is_update_step(tp)
                     loss = self.train_step(batch)
                     self.loss_history.append(loss)
+                    self._micro_losses.append(loss)
+                    if update:   # GenericTrainer.py:719-733 (values resolved at the next log point)
+                        self.model_setup.report_to_tensorboard(self.model, cfg, self.lr_scheduler, self.tensorboard)
+                        self._update_losses.append((gs, self._micro_losses))
+                        self._micro_losses = []
                     steps += 1
                     if steps == 1:
                         # long-lived objects (model, plans, workspaces) out of the collector's generations; cyclic
@@ -337,6 +350,8 @@ class GenericTrainer(TimedActionMixin):
         finally:
             if failed and self.world > 1:
                 self.abort_distributed()
+            elif not failed and log_every and steps % log_every:
+                self._report_losses(steps % log_every)   # the tail since the last log point
             if frozen:
                 gc.unfreeze()
             gc.enable()
@@ -350,14 +365,48 @@ class GenericTrainer(TimedActionMixin):
         self.world = 1
         abort()
 
+    def _open_scalar_log(self):
+        """<workspace>/tensorboard/<prefix><timestamp> (GenericTrainer.py:66-68); rank 0 writes."""
+        import os
+        from datetime import datetime
+
+        from ..util.tensorboard import ScalarLog
+        cfg = self.config
+        name = f"{cfg.save_filename_prefix}{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}"
+        return ScalarLog(os.path.join(cfg.workspace_dir, "tensorboard", name), enabled=self.rank == 0)
+
     def _report_losses(self, n: int):
-        vals = torch.stack(self.loss_history[-n:]).float()
+        """the log point: the mean of the last n micro-step losses printed, and per completed update step
+        `loss/train_step` (the sum of its micro-step losses) and `smooth_loss/train_step` (the EMA with decay
+        min(0.99, 1 - 1/k)) as GenericTrainer.py:722-732 computes them, all read in one device->host copy
+        (averaged over ranks under data parallel)."""
+        ups = self._update_losses
+        flat = self.loss_history[-n:] + [l for _, ls in ups for l in ls]
+        vals = torch.stack(flat).float()
         if self.world > 1:
             torch.distributed.all_reduce(vals)
             vals /= self.world
+        host = vals.tolist()
         if self.rank == 0:
-            print(f"step {self.model.train_progress.global_step}: loss {vals.mean().item():.5f} "
+            print(f"step {self.model.train_progress.global_step}: loss {sum(host[:n]) / n:.5f} "
                   f"lr {self.lr_scheduler.get_last_lr()[0]:.3e}", flush=True)
+        i = n
+        tb = self.tensorboard
+        for gs, ls in ups:
+            acc = 0.0
+            for v in host[i:i + len(ls)]:
+                acc += v
+            i += len(ls)
+            self._ema_loss = self._ema_loss or acc
+            self._ema_loss_steps += 1
+            decay = min(0.99, 1 - (1 / self._ema_loss_steps))
+            self._ema_loss = (self._ema_loss * decay) + (acc * (1 - decay))
+            if tb is not None:
+                tb.add_scalar("loss/train_step", acc, gs)
+                tb.add_scalar("smooth_loss/train_step", self._ema_loss, gs)
+        self._update_losses = []
+        if tb is not None:
+            tb.flush()
         del self.loss_history[:-n]
 
     def end(self):
@@ -366,6 +415,8 @@ class GenericTrainer(TimedActionMixin):
         output_model_format / output_dtype (rank 0 writes)."""
         if torch.cuda.is_available():
             torch.cuda.synchronize()
+        if self.tensorboard is not None:
+            self.tensorboard.close()
         if not self.one_step_trained:
             return None
         cfg = self.config

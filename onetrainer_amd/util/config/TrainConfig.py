@@ -55,6 +55,7 @@ class TrainConfig:
     learning_rate_warmup_steps: float = 200.0
     learning_rate_cycles: float = 1.0
     learning_rate_min_factor: float = 0.0
+    learning_rate_scaler: str = "NONE"
     clip_grad_norm: float | None = 1.0
     # noise / timesteps (ModelSetupNoiseMixin)
     offset_noise_weight: float = 0.0

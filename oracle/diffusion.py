@@ -32,11 +32,22 @@ def coefficients(betas):
 
 def create_noise(shape, generator, dtype=torch.float32, offset_noise_weight=0.0, perturbation_noise_weight=0.0):
     noise = torch.randn(shape, generator=generator, dtype=dtype)
+    off = pert = None
     if offset_noise_weight > 0:
         off = torch.randn((shape[0], shape[1], *[1] * (len(shape) - 2)), generator=generator, dtype=dtype)
-        noise = noise + offset_noise_weight * off
     if perturbation_noise_weight > 0:
-        noise = noise + perturbation_noise_weight * torch.randn(shape, generator=generator, dtype=dtype)
+        pert = torch.randn(shape, generator=generator, dtype=dtype)
+    return compose_noise(noise, off, pert, offset_noise_weight, perturbation_noise_weight)
+
+
+def compose_noise(noise, offset_draw, perturbation_draw, offset_noise_weight=0.0, perturbation_noise_weight=0.0):
+    """_create_noise's two optional terms (ModelSetupNoiseMixin.py:31-46) on given draws, in the reference's op
+    order and dtype: noise + (w * offset) with the offset [B, C, 1.., 1] broadcast over the pixels, then
+    noise + (w * perturbation)."""
+    if offset_noise_weight > 0:
+        noise = noise + (offset_noise_weight * offset_draw)
+    if perturbation_noise_weight > 0:
+        noise = noise + (perturbation_noise_weight * perturbation_draw)
     return noise
 
 

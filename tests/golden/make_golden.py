@@ -74,6 +74,17 @@ def main():
     p = DiffProbe()
     rec["timestep_deterministic"] = p._get_timestep_discrete(1000, True, torch.Generator().manual_seed(0), 4, cfg).numpy()
 
+    # ---- 1a. offset / perturbation noise terms (_create_noise with the weights > 0), f32 and bf16 sources ----
+    for wname, ow, pw in (("off", 0.1, 0.0), ("pert", 0.0, 0.2), ("both", 0.35, 0.05)):
+        for dname, dt in (("f32", torch.float32), ("bf16", torch.bfloat16)):
+            c = TrainConfig.default_values()
+            c.train_device = "cpu"
+            c.offset_noise_weight, c.perturbation_noise_weight = ow, pw
+            g = torch.Generator(device="cpu").manual_seed(11)
+            noise = DiffProbe()._create_noise(torch.zeros(3, 4, 8, 8, dtype=dt), c, g)
+            rec[f"noisex_{wname}_{dname}"] = bf16_bits(noise) if dt == torch.bfloat16 else noise.numpy()
+            rec[f"noisex_{wname}_w"] = np.array([ow, pw], dtype=np.float64)
+
     # ---- 1b. timestep transform on recorded draws (feeds the HIP kernel's injected-draw path) ---------
     # the draw the reference makes inside _get_timestep_discrete is re-made from the same seed
     # (torch.rand / torch.normal with the same generator state), then the reference maps it

@@ -145,6 +145,7 @@ def _worker_dead_peer(rank, world, port, q):
         os._exit(0)          # dies without a word
     cfg = TrainConfig.default_values()
     cfg.backup_after_unit = "NEVER"
+    cfg.workspace_dir = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"otamd_dead_peer_{os.getpid()}")
     tp = TrainProgress()
     loader = SimpleNamespace(get_data_set=lambda: SimpleNamespace(start_next_epoch=lambda: None),
                              get_data_loader=lambda: iter(range(3)))

@@ -228,6 +228,26 @@ def test_noise_and_timesteps(dev):
     assert torch.equal(tg[4:], K.timesteps(4, seed=5, sample0=4, device=dev))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, BF])
+@pytest.mark.parametrize("ow,pw", [(0.0, 0.0), (0.1, 0.0), (0.0, 0.2), (0.35, 0.05)])
+def test_noise_offset_perturbation(dev, dtype, ow, pw):
+    """offset / perturbation noise (ModelSetupNoiseMixin.py:31-46): the fused kernel equals the oracle's
+    composition of the raw Philox streams (1 noise, 4 offset per sample and channel, 5 perturbation) in the
+    reference's op order, bit for bit, for a rank-local slice of a global batch"""
+    from oracle.diffusion import compose_noise
+    B, H, W, C = 3, 8, 12, 4
+    seed, s0 = 21, 2
+    n, off = B * H * W * C, s0 * H * W * C
+    got = K.noise_ex((B, H, W, C), seed=seed, offset=off, offset_weight=ow, perturbation_weight=pw, dtype=dtype,
+                     device=dev)
+    base = K.noise_stream(n, seed, 1, offset=off, dtype=dtype, device=dev).view(B, H, W, C)
+    assert torch.equal(base, K.noise((B, H, W, C), seed=seed, offset=off, dtype=dtype, device=dev))
+    o = K.noise_stream((s0 + B) * C, seed, 4, dtype=dtype, device=dev)[s0 * C:].view(B, 1, 1, C)
+    p = K.noise_stream(n, seed, 5, offset=off, dtype=dtype, device=dev).view(B, H, W, C)
+    ref = compose_noise(base.cpu(), o.cpu(), p.cpu(), ow, pw)
+    assert torch.equal(got.cpu(), ref)
+
+
 def _coeffs(dev):
     betas = torch.linspace(0.00085 ** 0.5, 0.012 ** 0.5, 1000, dtype=torch.float32) ** 2
     acp = torch.cumprod(1 - betas, 0)

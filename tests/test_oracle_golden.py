@@ -27,6 +27,19 @@ def test_noise_and_timesteps(seed, dist):
     assert np.array_equal(OD.timestep_continuous(4, g2, **DISTS[dist]).numpy(), G[f"tcont_{dist}_{seed}"])
 
 
+@pytest.mark.parametrize("wname", ["off", "pert", "both"])
+@pytest.mark.parametrize("dname", ["f32", "bf16"])
+def test_offset_perturbation_noise(wname, dname):
+    """oracle create_noise (-> compose_noise, which the GPU test pins the fused kernel to) equals the
+    reference's _create_noise with offset / perturbation weights, bit for bit"""
+    ow, pw = (float(x) for x in G[f"noisex_{wname}_w"])
+    dt = torch.float32 if dname == "f32" else torch.bfloat16
+    g = torch.Generator().manual_seed(11)
+    noise = OD.create_noise((3, 4, 8, 8), g, dtype=dt, offset_noise_weight=ow, perturbation_noise_weight=pw)
+    got = noise.numpy() if dname == "f32" else noise.view(torch.int16).numpy().astype(np.uint16)
+    assert np.array_equal(got, G[f"noisex_{wname}_{dname}"])
+
+
 def test_deterministic_timestep():
     assert np.array_equal(OD.timestep_discrete(1000, 4, None, deterministic=True).numpy(), G["timestep_deterministic"])
 

@@ -136,6 +136,26 @@ def test_dp_noise_slices_match_global(dev):
     assert torch.equal(K.noise((2, 16, 16, 4), seed=9, offset=off, dtype=torch.float32, device=dev), g[2:])
 
 
+def test_offset_perturbation_noise_step(dev):
+    """with offset / perturbation noise on (ModelSetupNoiseMixin.py:31-46) predict() draws the fused noise_ex
+    noise (pinned to the reference's composition in test_kernels_gpu) and the step trains"""
+    cfg = TrainConfig.default_values()
+    cfg.batch_size = 2
+    cfg.offset_noise_weight, cfg.perturbation_noise_weight = 0.1, 0.05
+    model = create.create_model(cfg, dev, seed=3, unet_config=U.tiny_sdxl_config())
+    tr = GenericTrainer(cfg, model=model)
+    tr.start()
+    batch = synthetic_sdxl_batch(2, 128, 128, dev, seed=1, te1_dim=48, te2_dim=48, pooled_dim=64)
+    gs = model.train_progress.global_step
+    noise, _ = tr.model_setup.step_inputs(model, batch, cfg, model.train_progress)
+    shape = tuple(noise.shape)
+    assert torch.equal(noise, K.noise_ex(shape, seed=gs, offset_weight=0.1, perturbation_weight=0.05, dtype=noise.dtype,
+                                         device=dev))
+    assert not torch.equal(noise, K.noise(shape, seed=gs, dtype=noise.dtype, device=dev))
+    losses = [tr.train_step(batch).item() for _ in range(2)]
+    assert all(l == l and abs(l) < 1e4 for l in losses), losses
+
+
 def test_step_graph_matches_eager(dev, monkeypatch):
     """the captured + replayed step (trainer/step_graph.py) is bit-identical to the eager step:
     losses, every parameter and the AdamW moments over 4 steps, with a second batch shape in the

@@ -56,6 +56,11 @@ def test_config_defaults_match_reference():
         assert getattr(d, k) == v, k
 
 
+@pytest.fixture(autouse=True)
+def _in_tmp(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)   # train() opens its scalar log under the (relative) workspace_dir
+
+
 class _Loader:
     def __init__(self, n):
         self.n = n
@@ -86,6 +91,8 @@ def _trainer(ga=1, epochs=2, steps=6, **cfg_kw):
         return torch.zeros(())
 
     tr.train_step = step
+    tr.model_setup = SimpleNamespace(report_to_tensorboard=lambda m, c, sch, tb: log.append(("report", tp.global_step)))
+    tr.lr_scheduler = SimpleNamespace(get_last_lr=lambda: [1e-4])
     tr.backup = lambda t=None: log.append(("backup", tp.global_step))
     tr.save = lambda t=None: log.append(("save", tp.global_step))
     return tr, log
@@ -180,3 +187,57 @@ def test_end_without_backup_to_a_file(tmp_path):
     tr.train(log_every=0)
     tr.end()
     assert written == [dest] and _actions(log, "backup") == []
+
+
+def test_loss_and_smooth_loss_scalars():
+    """GenericTrainer.py:719-732: per update step `loss/train_step` = the sum of its micro-step losses and
+    `smooth_loss/train_step` = EMA with decay min(0.99, 1 - 1/k), at the update micro-step's global_step;
+    report_to_tensorboard once per update step"""
+    from onetrainer_amd.util.tensorboard import read_scalars
+    tr, log = _trainer(ga=2, epochs=1, steps=6)
+    tp = tr.model.train_progress
+    orig = tr.train_step
+
+    def step(batch):
+        v = float(tp.global_step)
+        orig(batch)
+        return torch.tensor(v)
+
+    tr.train_step = step
+    tr.train(log_every=4)
+    assert _actions(log, "report") == [2, 4, 6]          # after the update step's next_step()
+    rows = read_scalars(tr.tensorboard.log_dir)
+    loss = [(r["step"], r["value"]) for r in rows if r["tag"] == "loss/train_step"]
+    smooth = [(r["step"], r["value"]) for r in rows if r["tag"] == "smooth_loss/train_step"]
+    assert loss == [(1, 1.0), (3, 5.0), (5, 9.0)]
+    assert [st for st, _ in smooth] == [1, 3, 5] and [v for _, v in smooth] == pytest.approx([1.0, 3.0, 5.0])
+    tr.end()
+
+
+def test_report_learning_rates():
+    """BaseModelSetup.report_to_tensorboard (BaseModelSetup.py:96-119): lr/<display-name prefix>, first group wins"""
+    from onetrainer_amd.modelSetup.BaseStableDiffusionXLSetup import report_learning_rates
+    from onetrainer_amd.util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
+    pgc = NamedParameterGroupCollection()
+    for name in ("unet", "te/1", "te/2"):
+        pgc.add_group(NamedParameterGroup(name, [], 1.0, display_name=name))
+    got = []
+    tb = SimpleNamespace(add_scalar=lambda tag, v, step: got.append((tag, v, step)))
+    model = SimpleNamespace(parameters=pgc, train_progress=SimpleNamespace(global_step=7))
+    report_learning_rates(model, SimpleNamespace(get_last_lr=lambda: [1.0, 2.0, 3.0]), tb)
+    assert got == [("lr/unet", 1.0, 7), ("lr/te", 2.0, 7)]
+
+
+@pytest.mark.parametrize("scaler,factor", [("NONE", 1.0), ("BATCH", 2.0), ("GRADIENT_ACCUMULATION", 2 ** 0.5),
+                                           ("BOTH", 8 ** 0.5)])
+def test_learning_rate_scaler(scaler, factor):
+    """NamedParameterGroup.py:36-60: lr x sqrt(batch_size x GA) as learning_rate_scaler selects"""
+    from onetrainer_amd.util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
+    cfg = TrainConfig.default_values()
+    cfg.batch_size, cfg.gradient_accumulation_steps, cfg.learning_rate_scaler = 4, 2, scaler
+    pgc = NamedParameterGroupCollection()
+    pgc.add_group(NamedParameterGroup("unet", [], None))
+    pgc.add_group(NamedParameterGroup("te", [], 1e-5))
+    g = pgc.parameters_for_optimizer(cfg)
+    assert g[0]["lr"] == pytest.approx(cfg.learning_rate * factor) and g[0]["initial_lr"] == g[0]["lr"]
+    assert g[1]["lr"] == pytest.approx(1e-5 * factor)
