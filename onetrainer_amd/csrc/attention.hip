@@ -18,8 +18,9 @@
 // on the source address; one s_barrier per tile (RAW for tile t, WAR for the stage refilled
 // with tile t+NS-1).  Out-of-range rows / padded head columns are zero-filled by the
 // descriptor range check or an invalid offset.
-// Softmax VALU is kept under the MFMA time: packed fp32 math (v_pk_fma/mul), key masking only
-// on the partial last tile, and the forward's O rescale skipped when no lane's max grew.
+// Softmax VALU is kept under the MFMA time: single-issue fp32 math (no v_pk_*: they cost more than two
+// single ops beside MFMAs), key masking only on the partial last tile, and the forward's O rescale skipped
+// when no lane's max grew.
 #include "common.h"
 
 #include <cstring>
@@ -47,7 +48,6 @@ static constexpr float LOG2E = 1.4426950408889634f;
 
 typedef __attribute__((address_space(3))) short4v lds_s4;
 typedef __attribute__((address_space(3))) void lds_void_t;
-typedef float f2v __attribute__((ext_vector_type(2)));
 
 #define MEMBAR() asm volatile("" ::: "memory")
 #define BARRIER()                 \
@@ -213,8 +213,19 @@ __device__ __forceinline__ void load_row_frags(bf16x8 (&f)[D / 16], const bf16_t
   }
 }
 
-// P^T = exp2(S^T c - bias) in place, packed (v_pk_fma_f32 + v_exp_f32); masked keys already -inf
+// P^T = exp2(S^T c - bias) in place (v_fma_f32 + v_exp_f32); masked keys already -inf.  Single-issue f32
+// math throughout the softmax: beside MFMAs a packed v_pk_fma_f32 costs more than the two v_fma_f32 it
+// replaces (MI355X_MICROARCH.md, per-instruction constants), and the file is built with -fno-slp-vectorize
+// so the compiler does not re-pack it.
 __device__ __forceinline__ void exp2_scaled(float16v& S, float c, float bias) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) S[i] = __builtin_amdgcn_exp2f(fmaf(S[i], c, -bias));
+}
+// The D = 128 backward kernels keep the packed form (v_pk_fma_f32 / v_pk_mul_f32): at one wave per SIMD
+// (dK/dV) the single-issue form measured slower (Flux bwd 1274 -> 1414 us), while D = 64 gained 3-18 %
+// (profiles/r3_attn_scalar_ab.txt).  Same operations and rounding either way: bit-identical results.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void exp2_scaled_pk(float16v& S, float c, float bias) {
   const f2v c2 = {c, c}, nb = {-bias, -bias};
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -222,6 +233,16 @@ __device__ __forceinline__ void exp2_scaled(float16v& S, float c, float bias) {
     x = x * c2 + nb;
     S[2 * k] = __builtin_amdgcn_exp2f(x.x);
     S[2 * k + 1] = __builtin_amdgcn_exp2f(x.y);
+  }
+}
+__device__ __forceinline__ void dS_pk(float16v& S, const float16v& dP, float dlt) {
+  const f2v dl2 = {dlt, dlt};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    f2v p = {S[2 * k], S[2 * k + 1]}, d = {dP[2 * k], dP[2 * k + 1]};
+    p = p * (d - dl2);
+    S[2 * k] = p.x;
+    S[2 * k + 1] = p.y;
   }
 }
 
@@ -299,24 +320,40 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
       if (__builtin_amdgcn_ballot_w64(mc > m) != 0) {   // wave-uniform: some row max grew
         const float mn = fmaxf(m, mc);
         const float alpha = __builtin_amdgcn_exp2f(m - mn);
-        const f2v a2 = {alpha, alpha};
         l *= alpha;
+        if constexpr (D == 64) {
 #pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt)
+          for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            f2v o = {O[dt][2 * k], O[dt][2 * k + 1]};
-            o *= a2;
-            O[dt][2 * k] = o.x;
-            O[dt][2 * k + 1] = o.y;
-          }
+            for (int i = 0; i < 16; ++i) O[dt][i] *= alpha;
+        } else {
+          const f2v a2 = {alpha, alpha};
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              f2v o = {O[dt][2 * k], O[dt][2 * k + 1]};
+              o *= a2;
+              O[dt][2 * k] = o.x;
+              O[dt][2 * k + 1] = o.y;
+            }
+        }
         m = mn;
       }
-      exp2_scaled(S, c, m);
-      f2v rs2 = {S[0], S[1]};
+      float rs;
+      if constexpr (D == 64) {
+        exp2_scaled(S, c, m);
+        float r0 = S[0], r1 = S[1];   // two independent add chains
 #pragma unroll
-      for (int k = 1; k < 8; ++k) rs2 += f2v{S[2 * k], S[2 * k + 1]};
-      float rs = rs2.x + rs2.y;
+        for (int k = 1; k < 8; ++k) { r0 += S[2 * k]; r1 += S[2 * k + 1]; }
+        rs = r0 + r1;
+      } else {
+        exp2_scaled_pk(S, c, m);
+        f2v rs2 = {S[0], S[1]};
+#pragma unroll
+        for (int k = 1; k < 8; ++k) rs2 += f2v{S[2 * k], S[2 * k + 1]};
+        rs = rs2.x + rs2.y;
+      }
       rs += xor32(rs);
       l += rs;
       const bf16x8 p0 = pack_acc(S, 0), p1 = pack_acc(S, 1);
@@ -398,7 +435,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) { consume(qf[s]); consume(gf[s]); }
   const float c = a.scale * LOG2E;
-  const f2v dl2 = {dlt, dlt};
 
   float16v dQ[D / 32];
 #pragma unroll
@@ -428,13 +464,13 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
         for (int i = 0; i < 16; ++i)
           if (kbase + acc_row(i, h) >= a.Nk) S[i] = -INFINITY;
       }
-      exp2_scaled(S, c, lse2);
+      if constexpr (D == 64) {
+        exp2_scaled(S, c, lse2);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {   // dS^T = P^T (dP^T - delta)
-        f2v p = {S[2 * k], S[2 * k + 1]}, d = {dP[2 * k], dP[2 * k + 1]};
-        p = p * (d - dl2);
-        S[2 * k] = p.x;
-        S[2 * k + 1] = p.y;
+        for (int i = 0; i < 16; ++i) S[i] *= dP[i] - dlt;   // dS^T = P^T (dP^T - delta)
+      } else {
+        exp2_scaled_pk(S, c, lse2);
+        dS_pk(S, dP, dlt);
       }
       const bf16x8 s0 = pack_acc(S, 0), s1 = pack_acc(S, 1);
 #pragma unroll
@@ -507,7 +543,6 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) { consume(kf[s]); consume(vf[s]); }
   const float c = a.scale * LOG2E;
-  const f2v c2 = {c, c};
 
   float16v dK[D / 32], dV[D / 32];
 #pragma unroll
@@ -533,16 +568,26 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const float4 pp = e ? p23 : p01;
-        f2v x = {S[4 * g + 2 * e], S[4 * g + 2 * e + 1]};
-        const f2v ls = {pp.x, pp.z}, dl = {pp.y, pp.w};
-        x = x * c2 - ls;
-        f2v p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-        f2v d = {dP[4 * g + 2 * e], dP[4 * g + 2 * e + 1]};
-        d = p * (d - dl);
-        S[4 * g + 2 * e] = p.x;
-        S[4 * g + 2 * e + 1] = p.y;
-        dP[4 * g + 2 * e] = d.x;
-        dP[4 * g + 2 * e + 1] = d.y;
+        const int i0 = 4 * g + 2 * e;
+        if constexpr (D == 64) {
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(S[i0], c, -pp.x));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(S[i0 + 1], c, -pp.z));
+          dP[i0] = p0 * (dP[i0] - pp.y);
+          dP[i0 + 1] = p1 * (dP[i0 + 1] - pp.w);
+          S[i0] = p0;
+          S[i0 + 1] = p1;
+        } else {   // packed (see exp2_scaled_pk)
+          f2v x = {S[i0], S[i0 + 1]};
+          const f2v ls = {pp.x, pp.z}, dl = {pp.y, pp.w}, c2 = {c, c};
+          x = x * c2 - ls;
+          const f2v p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+          f2v d = {dP[i0], dP[i0 + 1]};
+          d = p * (d - dl);
+          S[i0] = p.x;
+          S[i0 + 1] = p.y;
+          dP[i0] = d.x;
+          dP[i0 + 1] = d.y;
+        }
       }
     }
     pk[0] = pack_acc(S, 0);

@@ -12,7 +12,7 @@ pids=()
 for f in "$W"/onetrainer_amd/csrc/*.hip; do
   b=$(basename "$f" .hip)
   extra=""
-  case "$b" in adamw|diffusion) extra="-ffp-contract=off";; attention) extra="-fno-honor-nans";; esac
+  case "$b" in adamw|diffusion) extra="-ffp-contract=off";; attention) extra="-fno-honor-nans -fno-slp-vectorize";; esac
   "$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -I "$W/onetrainer_amd/csrc" -c "$f" -o "$W/obj/$b.o" $extra &
   pids+=($!)
 done
