@@ -537,7 +537,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
     if ((lane >> 4) == wave) {   // 64 floats: lse of the tile's 32 queries, then their -delta; wave w moves 16w..
       const int qi = lane & 31;
       const unsigned off = (qt0 + qi < qend) ? (unsigned)(qt0 + qi) * 4u : OFF_INVALID;
-      dma4(wave < 2 ? rl : rn, st + 4 * TB, off);
+      if (wave < 2) dma4(rl, st + 4 * TB, off);   // (a wave-uniform branch: each descriptor stays in SGPRs)
+      else dma4(rn, st + 4 * TB, off);
     }
   };
 
