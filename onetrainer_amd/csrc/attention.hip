@@ -13,7 +13,7 @@
 //                  directly as the MFMA B operand; V^T comes from ds_read_b64_tr_b16.
 //   dK/dV        : S = Q K^T with the key on the lane; P and dS accumulators feed
 //                  dV^T = dO^T P and dK^T = Q^T dS directly; dO^T, Q^T by transposed LDS reads.
-// Staging: every streamed tile (K/V for fwd and dQ, Q/dO and the lse / -delta values for dK/dV)
+// Staging: every streamed tile (K/V for fwd and dQ, Q/dO and the {lse, delta} pairs for dK/dV)
 // goes HBM/L2 -> LDS by LDS-DMA (buffer_load ... lds) into an NS-deep ring, the swizzles applied
 // on the source address; one s_barrier per tile (RAW for tile t, WAR for the stage refilled
 // with tile t+NS-1).  Out-of-range rows / padded head columns are zero-filled by the
@@ -408,9 +408,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   load_row_frags<D>(gf, a.dout + b * a.bsdo + hh * a.Dv, a.lddo, q0, a.Nq, a.Dv);
   const int q = q0 + r;
   const long long srow = ((long long)b * a.H + hh) * a.Nq;
-  // delta = sum_d dO * O for this lane's query (the two half-waves split the head dim), published as
-  // -delta for the dK/dV kernel (launched next; it streams it beside the forward's lse): this replaces a
-  // separate delta pass over O and dO
+  // delta = sum_d dO * O for this lane's query (the two half-waves split the head dim), published
+  // with the forward's lse as the {lse, delta} pair the dK/dV kernel (launched next) streams: this
+  // replaces a separate delta pass over O and dO
   float dlt = 0.f, lse2 = 0.f;
   if (q < a.Nq) {
     const bf16_t* Op = a.o + b * a.bso + (long long)q * a.ldo + hh * a.Dv;
@@ -426,7 +426,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
     lse2 = a.lse[srow + q];
   }
   dlt += __shfl_xor(dlt, 32, 64);
-  if (h == 0 && q < a.Nq) const_cast<float*>(a.delta)[srow + q] = -dlt;
+  if (h == 0 && q < a.Nq) reinterpret_cast<float2*>(const_cast<float*>(a.delta))[srow + q] = make_float2(lse2, dlt);
   consume(dlt);
   consume(lse2);
 #pragma unroll
@@ -492,7 +492,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 }
 
 // dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of 32 in this split's range.
-// Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 lse and 32 -delta values.
+// Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 {lse, delta} pairs.
 // D = 128: the dK/dV accumulators alone take 128 VGPRs and the 3-deep ring (99 KiB) already limits a
 // CU to one block, so the full 512-entry register file is used instead of spilling at 256.
 // (A software-pipelined D = 128 variant -- S / dP of tile t+1 on the MFMA pipe during tile t's
@@ -503,7 +503,7 @@ template <int D, int OCC = 1>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = QT * D * 2;                 // one [32 x D] image
-  constexpr int STG = 4 * TB + QT * 8;           // + 32 lse + 32 -delta floats
+  constexpr int STG = 4 * TB + QT * 8;           // + 32 float2 pairs
   constexpr int NS = 3;                          // 50 KiB (D = 64): 3 blocks per CU
   using RImg = DmaImg<D, QT, false>;
   using TImg = DmaImg<D, QT, true>;
@@ -517,8 +517,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   const long long srow = ((long long)b * a.H + hh) * a.Nq;
   const auto rq = rsrc(a.q + b * a.bsq + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldq + a.Dv) * 2);
   const auto rg = rsrc(a.dout + b * a.bsdo + hh * a.Dv, ((long long)(a.Nq - 1) * a.lddo + a.Dv) * 2);
-  const auto rl = rsrc(a.lse + srow, (long long)a.Nq * 4);      // the forward's lse (log2 domain)
-  const auto rn = rsrc(a.delta + srow, (long long)a.Nq * 4);    // -delta, written by the dQ kernel
+  const auto rp = rsrc(a.delta + 2 * srow, (long long)a.Nq * 8);
   RImg ri;
   TImg ti;
   ri.prepare(wave, lane);
@@ -534,11 +533,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
     ti.issue(rq, st + TB, a.ldq, qt0, qend, a.Dv, wave);
     ri.issue(rg, st + 2 * TB, a.lddo, qt0, qend, a.Dv, wave);
     ti.issue(rg, st + 3 * TB, a.lddo, qt0, qend, a.Dv, wave);
-    if ((lane >> 4) == wave) {   // 64 floats: lse of the tile's 32 queries, then their -delta; wave w moves 16w..
-      const int qi = lane & 31;
-      const unsigned off = (qt0 + qi < qend) ? (unsigned)(qt0 + qi) * 4u : OFF_INVALID;
-      if (wave < 2) dma4(rl, st + 4 * TB, off);   // (a wave-uniform branch: each descriptor stays in SGPRs)
-      else dma4(rn, st + 4 * TB, off);
+    if ((lane >> 4) == wave) {   // 64 floats = 32 pairs; wave w moves floats 16w .. 16w+15
+      const unsigned off = (qt0 + (lane >> 1) < qend) ? (unsigned)(2 * qt0 + lane) * 4u : OFF_INVALID;
+      dma4(rp, st + 4 * TB, off);
     }
   };
 
@@ -556,51 +553,45 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) { dK[t] = zero16(); dV[t] = zero16(); }
 
-  // S = Q K^T and dP' = dO V^T - delta of one query tile (key on the lane): the dP chain starts from the
-  // tile's -delta values (registers 4g..4g+3 <-> queries 8g + 4h + 0..3: one 16-byte LDS read each), so
-  // dS = P dP' needs no subtraction per score
+  // S = Q K^T and dP = dO V^T of one query tile (key on the lane)
   auto sdp = [&](float16v& S_, float16v& dP_, const char* st) {
-    const float4* nd = reinterpret_cast<const float4*>(st + 4 * TB + 128);
     S_ = zero16();
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 v = nd[2 * g + h];
-      dP_[4 * g] = v.x; dP_[4 * g + 1] = v.y; dP_[4 * g + 2] = v.z; dP_[4 * g + 3] = v.w;
-    }
+    dP_ = zero16();
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       S_ = mfma32(lds_row_frag(st, D * 2, r, 2 * s + h), kf[s], S_);
       dP_ = mfma32(lds_row_frag(st + 2 * TB, D * 2, r, 2 * s + h), vf[s], dP_);
     }
   };
-  // P = exp2(S c - lse), dS = P dP', packed as the dV / dK B operands
+  // P = exp2(S c - lse), dS = P (dP - delta), packed as the dV / dK B operands
   auto softmax_pack = [&](float16v& S, float16v& dP, const char* st, bf16x8 (&pk)[4]) {
-    const float4* lv = reinterpret_cast<const float4*>(st + 4 * TB);   // lse of queries 4j .. 4j+3
+    const float4* pv = reinterpret_cast<const float4*>(st + 4 * TB);   // pv[j] = pairs 2j, 2j+1
 #pragma unroll
     for (int g = 0; g < 4; ++g) {      // registers 4g..4g+3 <-> queries 8g + 4h + (0..3)
-      const float4 l4 = lv[2 * g + h];
-      const float ls[4] = {l4.x, l4.y, l4.z, l4.w};
-      if constexpr (D == 64) {
+      const int q4 = 8 * g + 4 * h;
+      const float4 p01 = pv[q4 >> 1], p23 = pv[(q4 >> 1) + 1];   // {lse,dl} of q4, q4+1 | q4+2, q4+3
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(S[4 * g + e], c, -ls[e]));
-          dP[4 * g + e] *= p;
-          S[4 * g + e] = p;
-        }
-      } else {   // packed (see exp2_scaled_pk)
-        const f2v c2 = {c, c};
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          f2v x = {S[4 * g + e], S[4 * g + e + 1]};
-          const f2v l2 = {ls[e], ls[e + 1]};
-          x = x * c2 - l2;
+      for (int e = 0; e < 2; ++e) {
+        const float4 pp = e ? p23 : p01;
+        const int i0 = 4 * g + 2 * e;
+        if constexpr (D == 64) {
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(S[i0], c, -pp.x));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(S[i0 + 1], c, -pp.z));
+          dP[i0] = p0 * (dP[i0] - pp.y);
+          dP[i0 + 1] = p1 * (dP[i0 + 1] - pp.w);
+          S[i0] = p0;
+          S[i0 + 1] = p1;
+        } else {   // packed (see exp2_scaled_pk)
+          f2v x = {S[i0], S[i0 + 1]};
+          const f2v ls = {pp.x, pp.z}, dl = {pp.y, pp.w}, c2 = {c, c};
+          x = x * c2 - ls;
           const f2v p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-          f2v d = {dP[4 * g + e], dP[4 * g + e + 1]};
-          d = p * d;
-          S[4 * g + e] = p.x;
-          S[4 * g + e + 1] = p.y;
-          dP[4 * g + e] = d.x;
-          dP[4 * g + e + 1] = d.y;
+          f2v d = {dP[i0], dP[i0 + 1]};
+          d = p * (d - dl);
+          S[i0] = p.x;
+          S[i0 + 1] = p.y;
+          dP[i0] = d.x;
+          dP[i0 + 1] = d.y;
         }
       }
     }
@@ -737,7 +728,7 @@ static int attn_qsplit(const AttnArgs& a) {
   return qsplit;
 }
 
-// workspace bytes otamd_attn_bwd needs: -delta per query row (8 bytes reserved per row) + (split queries) fp32 dK/dV partials
+// workspace bytes otamd_attn_bwd needs: {lse, delta} pairs + (split queries) fp32 dK/dV partials
 OTAMD_API long long otamd_attn_bwd_ws_bytes(const AttnArgs* in) {
   if (!in || in->B <= 0 || in->H <= 0 || in->Nq <= 0 || in->Nk <= 0 || in->Dv <= 0) return -1;
   const long long nrow = (long long)in->B * in->H * in->Nq;
@@ -759,7 +750,7 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   const int qsplit = attn_qsplit(a);
   a.qsplit = qsplit;
   if (ws_bytes < otamd_attn_bwd_ws_bytes(in)) return OTAMD_EINVAL;
-  a.delta = ws;   // -delta per query row: written by the dQ kernel, read by dK/dV
+  a.delta = ws;   // {lse, delta} pairs: written by the dQ kernel, read by dK/dV
   if (qsplit > 1) {   // every slab element is written by exactly one block: no memset
     a.dk32 = ws + ((nrow * 2 + 64) / 64) * 64;
     a.dv32 = a.dk32 + (long long)qsplit * nkv;
