@@ -20,7 +20,8 @@ def rel_err(out, ref):
 
 
 @pytest.mark.parametrize("N,H,W,C,G,silu,eps", [(2, 16, 16, 320, 32, True, 1e-5), (2, 8, 8, 1280, 32, False, 1e-6),
-                                                (1, 32, 32, 960, 32, True, 1e-5), (3, 4, 4, 2560, 32, True, 1e-5)])
+                                                (1, 32, 32, 960, 32, True, 1e-5), (3, 4, 4, 2560, 32, True, 1e-5),
+                                                (4, 64, 64, 640, 32, True, 1e-6)])
 def test_groupnorm(dev, N, H, W, C, G, silu, eps):
     torch.manual_seed(0)
     x = rnd(N, H, W, C, dev=dev, scale=2.0, shift=0.5)
