@@ -101,7 +101,8 @@ long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_out);
 /* replaces: (plan override) the same GEMM with an explicit plan -- the autotuner's candidates and its
    cached per-shape choice (kernels.py set_gemm_autotune) and the measured plan table
    (onetrainer_amd/gemm_plans_mi355x.json).  tile: -1 v1 128x128, 0 256x256, 1 256x128, 2 128x256,
-   3 256x256/4 waves, 4 128x128/8 waves, 5 128x64, 6 64x128, 7 128x160, 8 256x160; splits >= 1;
+   3 256x256/4 waves, 4 128x128/8 waves, 5 128x64, 6 64x128, 7 128x160, 8 256x160, 9 / 10 = 5 / 6 on a
+   4-deep LDS ring; splits >= 1;
    workspace >= splits*M*N*4 bytes when splits > 1 */
 int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                         hipStream_t stream);

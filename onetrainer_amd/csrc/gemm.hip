@@ -536,11 +536,11 @@ OTAMD_API int otamd_gemm(const GemmArgs* in, int splits, void* workspace, long l
 
 // explicit plan (the autotuner's candidates and its cached choice): tile -1 = v1 128x128, 0 = 256x256,
 // 1 = 256x128, 2 = 128x256, 3 = 256x256 (4 waves), 4 = 128x128 (8 waves, 2 workgroups per CU),
-// 5 = 128x64, 6 = 64x128 (3 workgroups per CU), 7 = 128x160, 8 = 256x160;
+// 5 = 128x64, 6 = 64x128 (3 workgroups per CU), 7 = 128x160, 8 = 256x160, 9 / 10 = 5 / 6 on a 4-deep LDS ring;
 // splits >= 1 (rounded to whole 64-deep K steps)
 OTAMD_API int otamd_gemm_explicit(const GemmArgs* in, int tile, int splits, void* workspace, long long ws_bytes,
                                   hipStream_t stream) {
-  if (tile < -1 || tile > 8 || splits < 1) return OTAMD_EINVAL;
+  if (tile < -1 || tile > 10 || splits < 1) return OTAMD_EINVAL;
   return gemm_impl(in, splits, tile, workspace, ws_bytes, stream);
 }
 

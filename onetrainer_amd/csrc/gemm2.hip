@@ -2,12 +2,13 @@
 // gemm2_tiles_*.hip, one translation unit per tile family so they compile in parallel).
 #include "gemm2_kernel.h"
 
+#include <cstdlib>
 #include <mutex>
 #include <unordered_set>
 
 gemm2_fn gemm2_pick_a(int tile, int am, int bm, bool seg2, bool cs);   // 0, 3   256x256
 gemm2_fn gemm2_pick_b(int tile, int am, int bm, bool seg2, bool cs);   // 1, 2   256x128, 128x256
-gemm2_fn gemm2_pick_c(int tile, int am, int bm, bool seg2, bool cs);   // 4, 5, 6  128x128, 128x64, 64x128
+gemm2_fn gemm2_pick_c(int tile, int am, int bm, bool seg2, bool cs);   // 4, 5, 6, 9, 10  128x128, 128x64, 64x128
 gemm2_fn gemm2_pick_d(int tile, int am, int bm, bool seg2, bool cs);   // 7, 8   x160
 
 // byte extent an operand's gathers may touch (the DMA descriptor's range)
@@ -37,17 +38,21 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
     a2b = (unsigned)x;
     b2b = (unsigned)y;
   }
+  // OTAMD_SKINNY_NS4=1: tiles 5 / 6 run on the 4-deep ring (tiles 9 / 10) when they have no second K segment
+  static const bool skinny4 = [] { const char* e = getenv("OTAMD_SKINNY_NS4"); return e && e[0] == '1'; }();
+  if (skinny4 && (tile == 5 || tile == 6) && !seg2) tile += 4;
   switch (tile) {
     case 0: case 3: fn = gemm2_pick_a(tile, a.amode, a.bmode, seg2, cs); break;
     case 1: case 2: fn = gemm2_pick_b(tile, a.amode, a.bmode, seg2, cs); break;
-    case 4: case 5: case 6: fn = gemm2_pick_c(tile, a.amode, a.bmode, seg2, cs); break;
+    case 4: case 5: case 6: case 9: case 10: fn = gemm2_pick_c(tile, a.amode, a.bmode, seg2, cs); break;
     case 7: case 8: fn = gemm2_pick_d(tile, a.amode, a.bmode, seg2, cs); break;
     default: break;
   }
   // tile geometry: (BM, BN, waves, ring depth)
-  static const int geo[9][4] = {{256, 256, 8, 2}, {256, 128, 8, 2}, {128, 256, 8, 2}, {256, 256, 4, 2}, {128, 128, 8, 2},
-                                {128, 64, 8, 2},  {64, 128, 8, 2},  {128, 160, 8, 2}, {256, 160, 8, 2}};
-  if (tile >= 0 && tile < 9) { BMv = geo[tile][0]; BNv = geo[tile][1]; NWv = geo[tile][2]; NSv = geo[tile][3]; }
+  static const int geo[11][4] = {{256, 256, 8, 2}, {256, 128, 8, 2}, {128, 256, 8, 2}, {256, 256, 4, 2}, {128, 128, 8, 2},
+                                 {128, 64, 8, 2},  {64, 128, 8, 2},  {128, 160, 8, 2}, {256, 160, 8, 2}, {128, 64, 8, 4},
+                                 {64, 128, 8, 4}};
+  if (tile >= 0 && tile < 11) { BMv = geo[tile][0]; BNv = geo[tile][1]; NWv = geo[tile][2]; NSv = geo[tile][3]; }
   if (!fn) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
   const int lds = NSv * (BMv + BNv) * 128 + (cs && BMv == 256 ? (NWv * 64 / (BMv / 8)) * BMv * 4 : 0);

@@ -152,7 +152,27 @@ def _plan_table() -> dict:
             with open(_TABLE_PATH) as f:
                 for row in json.load(f)["plans"]:
                     _PLAN_TABLE[tuple(row["key"])] = (int(row["tile"]), int(row["splits"]))
+            if os.environ.get("OTAMD_SKINNY_SPLIT", "1") != "0":
+                _skinny_split(_PLAN_TABLE)
     return _PLAN_TABLE
+
+
+def _skinny_split(table: dict) -> None:
+    """Plan rule on top of the measured table (on by default; OTAMD_SKINNY_SPLIT=0 is the A/B switch): the LoRA
+    down-projections t = x A^T (K-mode A on the critical stream, N = rank or a fused group of ranks <= 128) planned
+    on a skinny tile without split-K fill under half the chip with one long K loop per workgroup; they get split-K
+    up to ~256 workgroups.
+    The table's plans were timed alone, where the reduce launch costs more than the idle CUs.  Same-box A/B
+    (profiles/r3_skinny_split_ab.txt): SDXL LoRA C4 128.8 -> 127.9 ms p50 (130.6 -> 128.3 mean); C3 unaffected."""
+    for key, (t, sp) in list(table.items()):
+        am, M, N, Kd = key[0], key[2], key[3], key[4]
+        if am != 0 or t not in (5, 6) or sp != 1 or N > 128:
+            continue
+        bm, bn = (128, 64) if t == 5 else (64, 128)
+        tiles = -(-M // bm) * -(-N // bn)
+        nk = -(-Kd // 64)
+        if tiles < 128 and nk >= 8:
+            table[key] = (t, max(2, min(8, nk // 4, 256 // max(1, tiles))))
 
 
 def plan_source() -> str:

@@ -138,10 +138,10 @@ def test_autotuned_plans(dev, autotune):
     assert len(K.gemm_autotune_cache()) == n
 
 
-@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_every_tile_explicit(dev, tile, monkeypatch):
     """every engine tile (4 = 128x128 with 8 waves, 2 workgroups per CU; 5 / 6 = 128x64 / 64x128; 7 / 8 = 128x160 /
-    256x160, 20 DMA pieces over 8 waves and 320-byte MN rows) through otamd_gemm_explicit: linear fwd (+bias +residual), dgrad, wgrad (split-K),
+    256x160, 20 DMA pieces over 8 waves and 320-byte MN rows; 9 / 10 = 5 / 6 on a 4-deep LDS ring) through otamd_gemm_explicit: linear fwd (+bias +residual), dgrad, wgrad (split-K),
     conv fwd / dgrad / wgrad, ragged sizes, and K of 1 to 5 K-steps (ring prologue and tail wait counts)."""
     torch.manual_seed(11)
     splits = {"v": 1}
