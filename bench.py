@@ -274,9 +274,13 @@ def main():
     t_start = time.perf_counter()
     evs[0].record(stream)
     losses = []
+    trace_alloc = os.environ.get("OTAMD_BENCH_ALLOC_TRACE") == "1"   # diagnostic: which timed steps grow the pool
     for i in range(args.steps):
         losses.append(tr.train_step(arb[order[args.warmup + i]] if sdxl_lora else batch))
         evs[i + 1].record(stream)
+        if trace_alloc:
+            log(f"[bench] timed step {i}: device allocs so far "
+                f"{torch.cuda.memory_stats(dev).get('num_device_alloc', 0) - ms0.get('num_device_alloc', 0)}")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
