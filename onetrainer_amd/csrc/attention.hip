@@ -303,6 +303,7 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
     const char* vimg = kimg + TB;
 #pragma unroll
     for (int sub = 0; sub < KT / 32; ++sub) {
+      if (t * KT + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile (Lk = 77): P = 0
       float16v S = zero16();
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) S = mfma32(lds_row_frag(kimg, D * 2, sub * 32 + r, 2 * s + h), qf[s], S);
@@ -455,6 +456,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
     const char* vrow = krow + 2 * TB;
 #pragma unroll
     for (int sub = 0; sub < KTD / 32; ++sub) {
+      if (t * KTD + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile: dS = 0
       // D = 64: dP^T starts from -delta (this lane's query: a per-lane constant vector built once), so
       // dS^T = P^T dP'^T needs no subtraction per score (the kernel is VALU-issue-bound at D = 64)
       float16v S = zero16(), dP = D == 64 ? ndl : zero16();
