@@ -221,9 +221,9 @@ __device__ __forceinline__ void exp2_scaled(float16v& S, float c, float bias) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) S[i] = __builtin_amdgcn_exp2f(fmaf(S[i], c, -bias));
 }
-// The D = 128 backward kernels keep the packed form (v_pk_fma_f32 / v_pk_mul_f32): at one wave per SIMD
-// (dK/dV) the single-issue form measured slower (Flux bwd 1274 -> 1414 us), while D = 64 gained 3-18 %
-// (profiles/r3_attn_scalar_ab.txt).  Same operations and rounding either way: bit-identical results.
+// The D = 128 forward and dK/dV kernels keep the packed form (v_pk_fma_f32 / v_pk_mul_f32): at one wave per
+// SIMD (dK/dV) the single-issue form measured slower (Flux bwd 1274 -> 1414 us), while D = 64 gained 3-18 % and
+// the D = 128 dQ kernel ~1 % (profiles/r3_attn_scalar_ab.txt).  Same operations and rounding either way.
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void exp2_scaled_pk(float16v& S, float c, float bias) {
   const f2v c2 = {c, c}, nb = {-bias, -bias};
@@ -235,16 +235,7 @@ __device__ __forceinline__ void exp2_scaled_pk(float16v& S, float c, float bias)
     S[2 * k + 1] = __builtin_amdgcn_exp2f(x.y);
   }
 }
-__device__ __forceinline__ void dS_pk(float16v& S, const float16v& dP, float dlt) {
-  const f2v dl2 = {dlt, dlt};
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    f2v p = {S[2 * k], S[2 * k + 1]}, d = {dP[2 * k], dP[2 * k + 1]};
-    p = p * (d - dl2);
-    S[2 * k] = p.x;
-    S[2 * k + 1] = p.y;
-  }
-}
+
 
 // ------------------------------------------------------------------------------------------
 // NS = LDS ring depth.  D = 128 runs NS = 2 (64 KiB): two blocks (8 waves) per CU instead of one
@@ -457,9 +448,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int sub = 0; sub < KTD / 32; ++sub) {
       if (t * KTD + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile: dS = 0
-      // D = 64: dP^T starts from -delta (this lane's query: a per-lane constant vector built once), so
-      // dS^T = P^T dP'^T needs no subtraction per score (the kernel is VALU-issue-bound at D = 64)
-      float16v S = zero16(), dP = D == 64 ? ndl : zero16();
+      // dP^T starts from -delta (this lane's query: a per-lane constant vector built once), so
+      // dS^T = P^T dP'^T needs no subtraction per score
+      float16v S = zero16(), dP = ndl;
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
         S = mfma32(lds_row_frag(krow, D * 2, sub * 32 + r, 2 * s + h), qf[s], S);
@@ -471,14 +462,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
         for (int i = 0; i < 16; ++i)
           if (kbase + acc_row(i, h) >= a.Nk) S[i] = -INFINITY;
       }
-      if constexpr (D == 64) {
-        exp2_scaled(S, c, lse2);
+      exp2_scaled(S, c, lse2);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) S[i] *= dP[i];   // dS^T = P^T (dP^T - delta)
-      } else {
-        exp2_scaled_pk(S, c, lse2);
-        dS_pk(S, dP, dlt);
-      }
+      for (int i = 0; i < 16; ++i) S[i] *= dP[i];   // dS^T = P^T (dP^T - delta)
       const bf16x8 s0 = pack_acc(S, 0), s1 = pack_acc(S, 1);
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
