@@ -162,3 +162,24 @@ def test_gemm_plan_table_wellformed():
         if r["key"][1] == 5 or r["key"][5]:   # conv-weight B / second K segment: v2 tiles only
             assert r["tile"] >= 0
     assert len(K._plan_table()) == len({tuple(r["key"]) for r in rows})
+
+
+def test_lora_down_projection_split_rule():
+    """kernels._skinny_split: only K-mode-A rows on the skinny tiles (5 / 6) without split-K, N <= 128, that fill
+    under 128 workgroups with >= 8 K-steps get split-K (up to ~256 workgroups, at most 8 splits)."""
+    from onetrainer_amd import kernels as K
+    z = (0,) * 11
+    t = {(0, 0, 4032, 32, 1280) + z: (6, 1),     # LoRA down-projection: 63 tiles, 20 K-steps -> 4 splits
+         (0, 1, 16128, 32, 640) + z: (5, 1),     # 127 tiles, 10 K-steps -> 2 splits
+         (0, 0, 4096, 96, 1280) + z: (6, 1),     # fused q|k|v ranks
+         (0, 0, 4096, 320, 1280) + z: (6, 1),    # N > 128: untouched
+         (1, 1, 32, 1280, 16384) + z: (6, 8),    # weight gradient (MN-mode A): untouched
+         (0, 0, 4096, 32, 320) + z: (6, 1),      # 5 K-steps: untouched
+         (0, 0, 4032, 32, 1280, 1) + (0,) * 10: (4, 1)}   # another tile: untouched
+    before = dict(t)
+    K._skinny_split(t)
+    assert t[(0, 0, 4032, 32, 1280) + z] == (6, 4)
+    assert t[(0, 1, 16128, 32, 640) + z] == (5, 2)
+    assert t[(0, 0, 4096, 96, 1280) + z] == (6, 4)
+    for k in list(before)[3:]:
+        assert t[k] == before[k], k
