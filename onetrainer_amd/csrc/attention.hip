@@ -710,11 +710,9 @@ OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
 }
 
 static int attn_qsplit(const AttnArgs& a) {
-  static const int target = [] { const char* e = getenv("OTAMD_QSPLIT_BLOCKS"); const int v = e ? atoi(e) : 512;
-                                  return v > 0 ? v : 512; }();   // A/B knob
   const int kblocks = (a.Nk + 127) / 128;
   int qsplit = 1;
-  while (kblocks * a.H * a.B * qsplit < target && qsplit < 64 && (a.Nq / (qsplit * 2)) >= 128) qsplit *= 2;
+  while (kblocks * a.H * a.B * qsplit < 512 && qsplit < 64 && (a.Nq / (qsplit * 2)) >= 128) qsplit *= 2;
   return qsplit;
 }
 
