@@ -496,6 +496,8 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   splits = (int)((a.K + kps - 1) / kps);
   a.k_per_split = (int)kps;
   if (splits > 1) {
+    // the split-K reduce indexes M * N in 32 bits: refuse before anything is launched
+    if ((long long)a.M * a.N >= (1LL << 32)) return OTAMD_EINVAL;
     if (!workspace || ws_bytes < otamd_gemm_ws_bytes(&a, splits) || !aligned16(workspace)) return OTAMD_EINVAL;
     a.slab = (float*)workspace;
     a.colsum_slab = a.colsum ? a.slab + (long long)splits * a.M * a.N : nullptr;
@@ -521,7 +523,6 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
     // 8-wide needs 16-byte aligned rows of C (bf16: ldc % 8, fp32 handled element-wise)
     const bool v8 = (a.N % 8) == 0 && (a.ldc % 8) == 0 && ((uintptr_t)a.C & 15) == 0;
     const long long nv = (long long)a.M * a.N / (v8 ? 8 : 4);
-    if ((long long)a.M * a.N >= (1LL << 32)) return OTAMD_EINVAL;
     const int blocks = (int)std::min<long long>((nv + 255) / 256, 8192);
     if (v8) splitk_reduce_kernel<8><<<blocks, 256, 0, stream>>>(a, splits);
     else splitk_reduce_kernel<4><<<blocks, 256, 0, stream>>>(a, splits);

@@ -14,6 +14,8 @@
 
 #include <array>
 #include <cstring>
+#include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -57,11 +59,16 @@ struct WsKey {
 struct WsHash {
   size_t operator()(const WsKey& k) const { return std::hash<int64_t>()(k.stream) * 31 + k.dev; }
 };
+// Launchers are thread-compatible (the reference runs the VAE and text encoders in data-loader worker threads,
+// DataLoaderMgdsMixin.py:47): the only mutable state is these two caches, each behind its own mutex.  A
+// workspace is reused in the order of its own stream, so threads driving different streams never share one.
+std::mutex g_ws_mu;
 std::unordered_map<WsKey, Tensor, WsHash> g_ws;
 
 void* workspace(int64_t nbytes, const at::Device& dev, int64_t stream) {
   if (nbytes <= 0) return nullptr;
   WsKey k{dev.index(), stream};
+  std::lock_guard<std::mutex> lk(g_ws_mu);
   auto it = g_ws.find(k);
   if (it == g_ws.end() || it->second.numel() < nbytes) {
     Tensor t = at::empty({std::max<int64_t>(nbytes, 64LL << 20)}, at::TensorOptions().dtype(at::kByte).device(dev));
@@ -80,7 +87,17 @@ struct PlanHash {
     return h;
   }
 };
+std::shared_mutex g_plans_mu;   // read per GEMM, written only when a table is loaded
 std::unordered_map<PlanKey, std::pair<int, int>, PlanHash> g_plans;
+
+bool lookup_plan(const PlanKey& k, int& tile, int& splits) {
+  std::shared_lock<std::shared_mutex> lk(g_plans_mu);
+  auto it = g_plans.find(k);
+  if (it == g_plans.end()) return false;
+  tile = it->second.first;
+  splits = it->second.second;
+  return true;
+}
 
 PlanKey tune_key(const GemmArgs& a) {
   return {a.amode, a.bmode, a.M, a.N, a.K, a.A2 ? a.K1 : 0, a.batch, a.c_f32, a.bias != nullptr, a.rowvec != nullptr,
@@ -94,14 +111,11 @@ int64_t ws_bytes(const GemmArgs& a, int s) {
 
 // kernels._gemm with splits == 0 (plan table, else the library's analytic plan) or an explicit split count
 void gemm(GemmArgs& a, int splits, const at::Device& dev, int64_t stream) {
-  if (splits == 0) {
-    auto it = g_plans.find(tune_key(a));
-    if (it != g_plans.end()) {
-      const int t = it->second.first, s = it->second.second;
-      const int64_t wb = ws_bytes(a, s);
-      check(otamd_gemm_explicit(&a, t, s, workspace(wb, dev, stream), wb, S(stream)), "otamd_gemm_explicit");
-      return;
-    }
+  int t = 0, s = 0;
+  if (splits == 0 && lookup_plan(tune_key(a), t, s)) {
+    const int64_t wb = ws_bytes(a, s);
+    check(otamd_gemm_explicit(&a, t, s, workspace(wb, dev, stream), wb, S(stream)), "otamd_gemm_explicit");
+    return;
   }
   int s_out = 0;
   const long long wb = otamd_gemm_plan(&a, splits, &s_out);
@@ -512,17 +526,25 @@ Tensor geglu_bwd(const Tensor& h, const Tensor& dout, int64_t stream) {
 }
 
 void set_plan_table(const std::vector<std::vector<int64_t>>& rows) {
-  g_plans.clear();
+  std::unordered_map<PlanKey, std::pair<int, int>, PlanHash> table;
   for (const auto& r : rows) {
     req(r.size() == 18, "plan table row: 16 key fields + tile + splits");
     PlanKey k;
     for (int i = 0; i < 16; ++i) k[i] = r[i];
-    g_plans[k] = {(int)r[16], (int)r[17]};
+    table[k] = {(int)r[16], (int)r[17]};
   }
+  std::unique_lock<std::shared_mutex> lk(g_plans_mu);
+  g_plans.swap(table);
 }
 
-int64_t plan_table_size() { return (int64_t)g_plans.size(); }
-void clear_workspaces() { g_ws.clear(); }
+int64_t plan_table_size() {
+  std::shared_lock<std::shared_mutex> lk(g_plans_mu);
+  return (int64_t)g_plans.size();
+}
+void clear_workspaces() {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  g_ws.clear();
+}
 
 }  // namespace
 

@@ -52,6 +52,8 @@ class GenericTrainer(TimedActionMixin):
         self.one_step_trained = False
         self._has_gradient = False
         self._wallclock_timers = False
+        self._ctl_group = None
+        self.agreements = 0
         self.rank, self.world = 0, 1
 
     # ------------------------------------------------------------------------------------------
@@ -255,11 +257,13 @@ class GenericTrainer(TimedActionMixin):
             model.optimizer.step()
             self.lr_scheduler.step()
             model.optimizer.zero_grad(set_to_none=True)
+            if self.tensorboard is not None:   # GenericTrainer.py:720-722: lr/* at this update's global_step
+                setup.report_to_tensorboard(model, cfg, self.lr_scheduler, self.tensorboard)
             setup.after_optimizer_step(model, cfg, tp)
+            self.one_step_trained = True      # GenericTrainer.py:749: only after an optimizer update
         else:
             store.accumulating = True
         self._has_gradient = not update
-        self.one_step_trained = True
         tp.next_step(cfg.batch_size)
         return loss.detach()
 
@@ -275,19 +279,30 @@ class GenericTrainer(TimedActionMixin):
         return (self.single_action_elapsed("save_skip_first", cfg.save_skip_first, cfg.save_every_unit, tp)
                 and self.repeating_action_needed("save", cfg.save_every, cfg.save_every_unit, tp, start_at_zero=False))
 
+    agree_every = 16   # update steps between the ranks' backup / save agreements under wall-clock timers
+
+    def _agreement_point(self, tp) -> bool:
+        """whether this (update-boundary) step consumes the backup / save commands.  Always in one process
+        or with only STEP / EPOCH timers (every rank raises the same commands at the same step); with a
+        wall-clock timer under data parallel only every `agree_every` update steps, where rank 0's decision
+        is broadcast (_agree), so the ranks do not meet on the host at every step."""
+        if self.world == 1 or not self._wallclock_timers:
+            return True
+        return (tp.global_step // self.config.gradient_accumulation_steps) % self.agree_every == 0
+
     def _agree(self, flags: int, step: int) -> int:
-        """Ranks must take a backup / save together (both barrier).  STEP / EPOCH timers agree by
-        construction; a wall-clock timer can fire on one rank and not another, so with one in use
-        rank 0's decision is published through the process group's store (host TCP, no device
-        sync) and every rank acts on it."""
+        """Ranks must take a backup / save together (both barrier).  A wall-clock timer can fire on one
+        rank and not another, so at an agreement point rank 0's flags are broadcast over a host-side gloo
+        group (no device sync, no keys left in the rendezvous store) and every rank acts on them."""
         if self.world == 1 or not self._wallclock_timers:
             return flags
-        store = torch.distributed.distributed_c10d._get_default_store()
-        key = f"otamd/actions/{step}"
-        if self.rank == 0:
-            store.set(key, str(flags))
-            return flags
-        return int(store.get(key).decode())
+        import torch.distributed as dist
+        if self._ctl_group is None:   # every rank reaches its first agreement point together
+            self._ctl_group = dist.new_group(backend="gloo")
+        t = torch.tensor([flags], dtype=torch.int64)
+        dist.broadcast(t, src=0, group=self._ctl_group)
+        self.agreements += 1
+        return int(t.item())
 
     def train(self, log_every: int = 10, max_steps: int | None = None):
         """GenericTrainer.py:600-749 around train_step(): backup_after / save_every timers raise the
@@ -300,6 +315,9 @@ class GenericTrainer(TimedActionMixin):
         self._wallclock_timers = any(TimedActionMixin._unit(u) in ("SECOND", "MINUTE", "HOUR")
                                      for u in (cfg.backup_after_unit, cfg.save_every_unit))
         steps = 0
+        # losses are read from the device every `flush_every` steps: printed when log_every is set, written as
+        # the loss scalars either way (the reference logs them every update step, GenericTrainer.py:723-733)
+        flush_every = log_every or 32
         frozen = False
         failed = True
         if self.tensorboard is None:
@@ -312,7 +330,7 @@ class GenericTrainer(TimedActionMixin):
                         self.commands.backup()
                     if self._needs_save(tp):
                         self.commands.save()
-                    if not self._has_gradient:
+                    if not self._has_gradient and self._agreement_point(tp):
                         flags = (int(self.commands.get_and_reset_backup_command())
                                  | int(self.commands.get_and_reset_save_command()) << 1)
                         flags = self._agree(flags, tp.global_step)
@@ -324,8 +342,7 @@ class GenericTrainer(TimedActionMixin):
                     loss = self.train_step(batch)
                     self.loss_history.append(loss)
                     self._micro_losses.append(loss)
-                    if update:   # GenericTrainer.py:719-733 (values resolved at the next log point)
-                        self.model_setup.report_to_tensorboard(self.model, cfg, self.lr_scheduler, self.tensorboard)
+                    if update:   # GenericTrainer.py:723-733 (values resolved at the next flush point)
                         self._update_losses.append((gs, self._micro_losses))
                         self._micro_losses = []
                     steps += 1
@@ -336,9 +353,9 @@ class GenericTrainer(TimedActionMixin):
                         gc.freeze()
                         gc.disable()
                         frozen = True
-                    if log_every and steps % log_every == 0:
+                    if steps % flush_every == 0:
                         gc.collect()
-                        self._report_losses(log_every)
+                        self._report_losses(flush_every, echo=bool(log_every))
                     if self.commands.get_stop_command() or (max_steps is not None and steps >= max_steps):
                         failed = False
                         return
@@ -350,8 +367,8 @@ class GenericTrainer(TimedActionMixin):
         finally:
             if failed and self.world > 1:
                 self.abort_distributed()
-            elif not failed and log_every and steps % log_every:
-                self._report_losses(steps % log_every)   # the tail since the last log point
+            elif not failed and steps % flush_every:
+                self._report_losses(steps % flush_every, echo=bool(log_every))   # the tail since the last flush
             if frozen:
                 gc.unfreeze()
             gc.enable()
@@ -375,7 +392,7 @@ class GenericTrainer(TimedActionMixin):
         name = f"{cfg.save_filename_prefix}{datetime.now().strftime('%Y-%m-%d_%H-%M-%S')}"
         return ScalarLog(os.path.join(cfg.workspace_dir, "tensorboard", name), enabled=self.rank == 0)
 
-    def _report_losses(self, n: int):
+    def _report_losses(self, n: int, echo: bool = True):
         """the log point: the mean of the last n micro-step losses printed, and per completed update step
         `loss/train_step` (the sum of its micro-step losses) and `smooth_loss/train_step` (the EMA with decay
         min(0.99, 1 - 1/k)) as GenericTrainer.py:722-732 computes them, all read in one device->host copy
@@ -387,7 +404,7 @@ class GenericTrainer(TimedActionMixin):
             torch.distributed.all_reduce(vals)
             vals /= self.world
         host = vals.tolist()
-        if self.rank == 0:
+        if self.rank == 0 and echo:
             print(f"step {self.model.train_progress.global_step}: loss {sum(host[:n]) / n:.5f} "
                   f"lr {self.lr_scheduler.get_last_lr()[0]:.3e}", flush=True)
         i = n

@@ -252,10 +252,12 @@ class OverlappedGradNorm:
             if cur and size + n > limit:
                 self.buckets.append((c_lo, c_hi, cur))
                 cur, size = [], 0
-            b, e = t_chunks.get(ti, (0, 0))
             if not cur:
-                c_lo, c_hi = b, e
-            c_lo, c_hi = min(c_lo, b), max(c_hi, e)
+                c_lo, c_hi = None, None
+            if ti in t_chunks:   # a tensor with no norm chunks (numel 0) must not stretch the bucket's range
+                b, e = t_chunks[ti]
+                c_lo = b if c_lo is None else min(c_lo, b)
+                c_hi = e if c_hi is None else max(c_hi, e)
             cur.append(name)
             size += n
         if cur:
@@ -278,6 +280,8 @@ class OverlappedGradNorm:
     def _launch(self, bi, side):
         self.launched[bi] = True
         c0, c1, _ = self.buckets[bi]
+        if c0 is None:   # only empty tensors: nothing to sum
+            return
         opt = self.opt
         g = opt.store.grad
         dtype = 0 if g.dtype == torch.bfloat16 else 1

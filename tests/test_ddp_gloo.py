@@ -178,3 +178,68 @@ def test_dead_peer_times_out_and_aborts():
         p.join(timeout=60)
     assert rank == 0 and msg.startswith("raised") and msg.endswith("group initialized: False"), msg
     assert all(p.exitcode is not None for p in procs)
+
+
+def _worker_wallclock(rank, world, port, q):
+    """a MINUTE backup timer under data parallel: rank 0's wall clock fires, rank 1's does not; both ranks
+    back up together, and the ranks meet on the host only every `agree_every` update steps (no per-step
+    rendezvous-store traffic, no keys left behind)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), OTAMD_DIST_BACKEND="gloo")
+    from types import SimpleNamespace
+
+    import onetrainer_amd.util.TimedActionMixin as TM
+    from onetrainer_amd.trainer import ddp
+    from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+    from onetrainer_amd.util.TrainProgress import TrainProgress
+    try:
+        ddp.init_from_env(timeout_s=60)
+        now = [1000.0]
+        TM.time.time = lambda: now[0]
+        cfg = TrainConfig.default_values()
+        cfg.backup_after, cfg.backup_after_unit = 1, "MINUTE"
+        cfg.workspace_dir = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"otamd_wallclock_{os.getpid()}")
+        tp = TrainProgress()
+        loader = SimpleNamespace(get_data_set=lambda: SimpleNamespace(start_next_epoch=lambda: None),
+                                 get_data_loader=lambda: iter(range(40)))
+        tr = GenericTrainer(cfg, model=SimpleNamespace(train_progress=tp), data_loader=loader)
+        tr.rank, tr.world = rank, world
+        backups = []
+        tr.backup = lambda t=None: backups.append(tp.global_step)
+        store = dist.distributed_c10d._get_default_store()
+        keys = {}
+
+        def step(batch):
+            if tp.global_step == 17:   # after the control group's one-time rendezvous and two agreements
+                keys[17] = store.num_keys()
+            if rank == 0:
+                now[0] += 61.0          # only rank 0's clock moves
+            dist.all_reduce(torch.ones(4))
+            tp.next_step(1)
+            return torch.zeros(())
+
+        tr.train_step = step
+        tr.train(log_every=0, max_steps=40)
+        assert tr.agreements == 3, tr.agreements          # update steps 0, 16, 32
+        assert backups == [16, 32], backups
+        assert store.num_keys() == keys[17], (store.num_keys(), keys)   # nothing written per step
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_wallclock_backup_agreement_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_wallclock, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res

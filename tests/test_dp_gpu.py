@@ -95,3 +95,21 @@ def test_dp4_ga2_bf16_vs_fp32_reduce(tmp_path):
     rel_bf16 = _compare(_run(tmp_path, 4, False, global_batch=4, ga=2), ref, False, "dp4 ga2 vs dp1 ga2")
     rel_fp32 = _compare(_run(tmp_path, 4, True, global_batch=4, ga=2), ref, True, "dp4 ga2 vs dp1 ga2")
     print(f"dp4 reduction error vs world 1: bf16 {rel_bf16:.3e}, fp32 staging {rel_fp32:.3e}")
+
+
+def test_rccl_reducer_world1(tmp_path):
+    """RCCL itself (torch.distributed 'nccl') under the bucketed reducer: a one-rank group on the box's GPU, the
+    all-reduces issued from inside backward on the issue stream; a one-rank sum is the identity, so the step must
+    be bit-identical to the plain step, in bf16 in place and through the fp32 staging copy
+    (tests/workers/rccl_world1.py)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "OTAMD_DIST_BACKEND"):
+        env.pop(k, None)
+    out = tmp_path / "rccl.pt"
+    p = subprocess.run([sys.executable, str(Path(__file__).parent / "workers" / "rccl_world1.py"), "--out", str(out)],
+                       env=env, timeout=240)
+    assert p.returncode == 0
+    r = torch.load(out, weights_only=True)
+    assert r["buckets"] > 3 and r["nonzero"]
+    assert r["grad_equal"] and r["param_equal"], r
+    assert r["grad_equal_fp32"] and r["param_equal_fp32"], r

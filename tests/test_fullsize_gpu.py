@@ -2,11 +2,13 @@
 
 Oracle comparisons at full width (oracle/unet.py, oracle/flux.py on the host CPU, fp32, same
 weights, same bf16-rounded inputs, same injected noise / timesteps):
-  * SDXL `sdxl_config()` (320/640/1280, depth [0,2,10], ctx 2048) at 512^2 b=1;
+  * SDXL `sdxl_config()` (320/640/1280, depth [0,2,10], ctx 2048) at 512^2 b=1 and at C3's own resolution,
+    1024^2 b=1 (level-1 self-attention over 4096 tokens, the step's hottest attention shape);
   * SD 1.5 `sd15_config()` (8 heads of 40/80/160, ctx 768) at 512^2 b=1 -- C1's shape;
   * FLUX.1 at full width (D = 3072, 24 x 128 heads, T5 ctx 4096) with 1 double + 1 single block at
     768^2 b=1 (2304 image tokens + 77 text tokens).
-  Each checks the diffusion loss to rtol 1e-3 (north star) and every parameter gradient's cosine.
+  Each checks the diffusion loss to rtol 1e-3 (north star), the prediction's element-wise cosine and every
+  parameter gradient's cosine.
 
 Full-size property steps at the BASELINE workloads (too large for a CPU oracle):
   * C2 SD 1.5 FT 512^2 b=16, C3 SDXL FT 1024^2 b=4 (per-rank batch of the DP-8 config),
@@ -52,21 +54,21 @@ def _free():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("name", ["sdxl", "sd15"])
-def test_full_unet_512_matches_oracle(dev, name):
+@pytest.mark.parametrize("name,res", [("sdxl", 512), ("sd15", 512), ("sdxl", 1024)])
+def test_full_unet_matches_oracle(dev, name, res):
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
     cfg = U.sdxl_config() if name == "sdxl" else U.sd15_config()
     m = U.UNet2DConditionModel(cfg, dev, seed=1)
     om = _oracle_unet(cfg, m)
     g = torch.Generator().manual_seed(0)
-    B, h = 1, 64
+    B, h = 1, res // 8
     x0 = torch.randn(B, 4, h, h, generator=g)
     eps = torch.randn(B, 4, h, h, generator=g)
     t = torch.tensor([517], dtype=torch.int32)
     ehs = torch.randn(B, 77, cfg.cross_attention_dim, generator=g).bfloat16()
     if cfg.addition_embed:
         te = torch.randn(B, 1280, generator=g).bfloat16()
-        tid = torch.tensor([[512., 512., 0., 0., 512., 512.]])
+        tid = torch.tensor([[float(res), float(res), 0., 0., float(res), float(res)]])
     else:
         te = tid = None
     xt = OD.add_noise_ddpm(x0, eps, t.long(), OD.scaled_linear_betas()).bfloat16()
@@ -77,8 +79,11 @@ def test_full_unet_512_matches_oracle(dev, name):
     loss, coef, _ = K.mse_loss(out, eps.permute(0, 2, 3, 1).contiguous().to(dev))
     ref = om(xt.float(), t.long(), ehs.float(), None if te is None else te.float(), tid)
     ref_loss = OD.diffusion_losses(ref, eps, torch.ones(B)).mean()
-    print(f"{name} 512^2 loss hip {loss.item():.6f} oracle {ref_loss.item():.6f}")
+    pred = out[..., :4].float().cpu().permute(0, 3, 1, 2)
+    pcos = _cos(pred, ref.detach())
+    print(f"{name} {res}^2 loss hip {loss.item():.6f} oracle {ref_loss.item():.6f} prediction cosine {pcos:.6f}")
     assert abs(loss.item() - ref_loss.item()) <= 1e-3 * abs(ref_loss.item())
+    assert pcos > 0.999, pcos
     m.store.begin_backward()
     out.backward(K.mse_grad(out, eps.permute(0, 2, 3, 1).contiguous().to(dev), coef))
     m.store.finish_backward()

@@ -183,3 +183,30 @@ def test_lora_down_projection_split_rule():
     assert t[(0, 0, 4096, 96, 1280) + z] == (6, 4)
     for k in list(before)[3:]:
         assert t[k] == before[k], k
+
+
+def test_overlapped_norm_buckets_skip_empty_tensors():
+    """OverlappedGradNorm bucket chunk ranges: a tensor with no norm chunks (numel 0) must not stretch a
+    bucket's range back to chunk 0 (every earlier tensor's chunks would be summed twice into the norm)."""
+    from types import SimpleNamespace
+
+    from onetrainer_amd.util.optimizer.adamw_fused import OverlappedGradNorm
+    numels = {"a": 70000, "b": 0, "c": 1000, "d": 0, "e": 5}
+    order = list(numels)
+    chunk_tensor = []
+    for ti, n in enumerate(order):
+        chunk_tensor += [ti] * ((numels[n] + (1 << 16) - 1) >> 16)
+    store = SimpleNamespace(order=order, slots={n: SimpleNamespace(numel=v) for n, v in numels.items()},
+                            grad=torch.zeros(1, dtype=torch.bfloat16), ready_hooks=[])
+    opt = SimpleNamespace(store=store, _chunk_tensor=chunk_tensor)
+    for bucket_bytes in (2, 20, 1 << 30):   # 20 B: e and the empty d share a bucket
+        ov = OverlappedGradNorm(opt, bucket_bytes=bucket_bytes)
+        covered = []
+        for c0, c1, names in ov.buckets:
+            if c0 is None:
+                assert all(numels[n] == 0 for n in names)
+                continue
+            want = [ci for ci, ti in enumerate(chunk_tensor) if order[ti] in names]
+            assert list(range(c0, c1)) == want, (c0, c1, names)
+            covered += want
+        assert sorted(covered) == list(range(len(chunk_tensor)))

@@ -91,7 +91,11 @@ def sdpa_ref(q, k, v, heads):
                                          (2, 2048, 2048, 4, 64), (1, 333, 1000, 2, 128), (1, 128, 50, 2, 64),
                                          (1, 192, 64, 2, 64), (1, 256, 128, 2, 64), (1, 200, 190, 2, 128),
                                          (1, 160, 3, 2, 64), (2, 1024, 96, 20, 64), (1, 100, 77, 3, 64),
-                                         (1, 1024, 97, 2, 64)])
+                                         (1, 1024, 97, 2, 64),
+                                         # the step's own shapes: SDXL 1024^2 b=4 level-1 self (the hottest) and
+                                         # cross, level-2 self and cross; FLUX.1 768^2 b=4 joint attention
+                                         (4, 4096, 4096, 10, 64), (4, 4096, 77, 10, 64), (4, 1024, 1024, 20, 64),
+                                         (4, 1024, 77, 20, 64), (4, 2381, 2381, 24, 128)])
 def test_attention(dev, B, Nq, Nk, H, D):
     torch.manual_seed(2)
     q, k, v = rnd(B, Nq, H * D, dev=dev), rnd(B, Nk, H * D, dev=dev), rnd(B, Nk, H * D, dev=dev)

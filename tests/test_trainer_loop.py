@@ -82,11 +82,13 @@ def _trainer(ga=1, epochs=2, steps=6, **cfg_kw):
     tr = GT.GenericTrainer(cfg, model=SimpleNamespace(train_progress=tp), data_loader=_Loader(steps))
     log = []
 
-    def step(batch):
+    def step(batch):   # the loop-visible effects of GenericTrainer.train_step
         update = tr._is_update_step(tp)
         log.append(("step", tp.global_step))
+        if update:
+            tr.model_setup.report_to_tensorboard(None, cfg, tr.lr_scheduler, tr.tensorboard)
+            tr.one_step_trained = True
         tr._has_gradient = not update
-        tr.one_step_trained = True
         tp.next_step(cfg.batch_size)
         return torch.zeros(())
 
@@ -205,7 +207,7 @@ def test_loss_and_smooth_loss_scalars():
 
     tr.train_step = step
     tr.train(log_every=4)
-    assert _actions(log, "report") == [2, 4, 6]          # after the update step's next_step()
+    assert _actions(log, "report") == [1, 3, 5]          # at the update step, before next_step()
     rows = read_scalars(tr.tensorboard.log_dir)
     loss = [(r["step"], r["value"]) for r in rows if r["tag"] == "loss/train_step"]
     smooth = [(r["step"], r["value"]) for r in rows if r["tag"] == "smooth_loss/train_step"]
@@ -241,3 +243,83 @@ def test_learning_rate_scaler(scaler, factor):
     g = pgc.parameters_for_optimizer(cfg)
     assert g[0]["lr"] == pytest.approx(cfg.learning_rate * factor) and g[0]["initial_lr"] == g[0]["lr"]
     assert g[1]["lr"] == pytest.approx(1e-5 * factor)
+
+
+class _FakeSetup:
+    """predict / calculate_loss / report hooks of a model setup over one scalar parameter (no GPU)"""
+
+    def __init__(self, tb_log):
+        self.tb_log = tb_log
+
+    def predict(self, model, batch, cfg, tp):
+        return {"p": model.w * 2.0}
+
+    def calculate_loss(self, model, batch, out, cfg):
+        return (out["p"] ** 2).sum()
+
+    def report_to_tensorboard(self, model, cfg, sch, tb):
+        from onetrainer_amd.modelSetup.BaseStableDiffusionXLSetup import report_learning_rates
+        report_learning_rates(model, sch, tb)
+
+    def after_optimizer_step(self, model, cfg, tp):
+        pass
+
+
+def _real_step_trainer(ga):
+    from onetrainer_amd.util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
+    cfg = TrainConfig.default_values()
+    cfg.gradient_accumulation_steps = ga
+    cfg.clip_grad_norm = None
+    tp = TrainProgress()
+    w = torch.nn.Parameter(torch.ones(()))
+    pgc = NamedParameterGroupCollection()
+    pgc.add_group(NamedParameterGroup("unet", [w], 1.0, display_name="unet"))
+    opt = torch.optim.SGD([w], lr=0.1)
+    store = SimpleNamespace(begin_backward=lambda: None, finish_backward=lambda: None, accumulating=False)
+    model = SimpleNamespace(w=w, optimizer=opt, train_progress=tp, train_store=store, parameters=pgc)
+    got = []
+    tr = GT.GenericTrainer(cfg, model=model, model_setup=_FakeSetup(got))
+    tr.lr_scheduler = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0)
+    tr.tensorboard = SimpleNamespace(add_scalar=lambda tag, v, st: got.append((tag, st)))
+    return tr, got
+
+
+def test_train_step_reports_lr_at_the_update_step():
+    """BaseModelSetup.report_to_tensorboard runs inside the update branch before train_progress.next_step
+    (GenericTrainer.py:720-754): lr/<group> carries the update step's own global_step, not the next one"""
+    tr, got = _real_step_trainer(ga=2)
+    for _ in range(4):
+        tr.train_step({})
+    assert got == [("lr/unet", 1), ("lr/unet", 3)]
+
+
+def test_one_step_trained_only_after_an_update():
+    """GenericTrainer.py:749: a micro-step without an optimizer update does not count as trained, so end()
+    after a stop inside the first accumulation window saves nothing"""
+    tr, _ = _real_step_trainer(ga=2)
+    tr.train_step({})
+    assert not tr.one_step_trained
+    tr.train_step({})
+    assert tr.one_step_trained
+
+
+def test_losses_flushed_without_log_every():
+    """train(log_every=0): the loss scalars are still written (every 32 steps and at the end) and the
+    device loss history stays bounded"""
+    from onetrainer_amd.util.tensorboard import read_scalars
+    tr, log = _trainer(epochs=1, steps=70)
+    tp = tr.model.train_progress
+    orig = tr.train_step
+
+    def step(batch):
+        v = float(tp.global_step)
+        orig(batch)
+        return torch.tensor(v)
+
+    tr.train_step = step
+    tr.train(log_every=0)
+    rows = read_scalars(tr.tensorboard.log_dir)
+    loss = [(r["step"], r["value"]) for r in rows if r["tag"] == "loss/train_step"]
+    assert loss == [(g, float(g)) for g in range(70)]
+    assert len(tr.loss_history) <= 32 and not tr._update_losses
+    tr.end()
