@@ -23,6 +23,7 @@
 // when no lane's max grew.
 #include "common.h"
 
+#include <algorithm>
 #include <cstring>
 #include <cstdlib>
 #include <mutex>
@@ -38,7 +39,7 @@ struct AttnArgs {
   int B, H, Nq, Nk, Dv;
   float scale;
   int qsplit;
-  int pad_;
+  int xcd;   // (the header's reserved pad_; callers pass 0) set by the launchers: XCD-grouped block order
 };
 
 #define KT 64   // keys per staged tile (fwd / dQ)
@@ -55,6 +56,13 @@ typedef __attribute__((address_space(3))) void lds_void_t;
     MEMBAR();                     \
     __builtin_amdgcn_s_barrier(); \
     MEMBAR();                     \
+  } while (0)
+
+// publishes this wave's ds_write results: s_barrier alone does not wait for them (cdna_hip_programming.md §5)
+#define BARRIER_LDS()                                     \
+  do {                                                    \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
+    BARRIER();                                            \
   } while (0)
 
 template <int N>
@@ -76,6 +84,27 @@ __device__ __forceinline__ void consume(const T& x) { asm volatile("" ::"v"(x));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+
+// Workgroup order (cdna_hip_programming.md T1): the hardware deals workgroup i (x fastest) to XCD i % 8, so the
+// blocks of one (batch, head) -- which all stream that head's K / V (forward, dQ) or Q / dO (dK/dV) tiles --
+// land on all 8 XCDs and each XCD's L2 fetches the same tiles.  With a.xcd set, the grid is renumbered so that
+// XCD x runs a contiguous range of (block, head, batch): one (batch, head)'s blocks share one L2 (bijective for
+// any count).
+__device__ __forceinline__ void block_ids(const AttnArgs& a, int& bx, int& by, int& bz) {
+  if (!a.xcd) {
+    bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    return;
+  }
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int total = nx * ny * gridDim.z;
+  const int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int x = lin & 7, j = lin >> 3, q = total >> 3, rr = total & 7;
+  const int n = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + j;
+  bx = n % nx;
+  const int t = n / nx;
+  by = t % ny;
+  bz = t / ny;
 }
 
 // row image: [rows][D] bf16, 16-byte chunk c of row r stored at c ^ (r & 7)
@@ -249,10 +278,11 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
   using KImg = DmaImg<D, KT, false>;
   using VImg = DmaImg<D, KT, true>;
   constexpr int LOADS = KImg::PW + VImg::PW;
-  const int b = blockIdx.z, hh = blockIdx.y;
+  int bx, hh, b;
+  block_ids(a, bx, hh, b);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = bx * 128 + wave * 32;
   const bf16_t* Q = a.q + b * a.bsq + hh * a.Dv;
   const auto rk = rsrc(a.k + b * a.bsk + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldk + a.Dv) * 2);
   const auto rv = rsrc(a.v + b * a.bsv + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldv + a.Dv) * 2);
@@ -378,10 +408,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   using RImg = DmaImg<D, KTD, false>;
   using TImg = DmaImg<D, KTD, true>;
   constexpr int LOADS = 2 * RImg::PW + TImg::PW;
-  const int b = blockIdx.z, hh = blockIdx.y;
+  int bx, hh, b;
+  block_ids(a, bx, hh, b);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = bx * 128 + wave * 32;
   const auto rk = rsrc(a.k + b * a.bsk + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldk + a.Dv) * 2);
   const auto rv = rsrc(a.v + b * a.bsv + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldv + a.Dv) * 2);
   RImg ri;
@@ -496,12 +527,12 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   using RImg = DmaImg<D, QT, false>;
   using TImg = DmaImg<D, QT, true>;
   constexpr int LOADS = 2 * RImg::PW + 2 * TImg::PW + 1;
-  const int bz = blockIdx.z;
+  int bx, hh, bz;
+  block_ids(a, bx, hh, bz);
   const int b = bz / a.qsplit, split = bz % a.qsplit;
-  const int hh = blockIdx.y;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int k0 = blockIdx.x * 128 + wave * 32;
+  const int k0 = bx * 128 + wave * 32;
   const long long srow = ((long long)b * a.H + hh) * a.Nq;
   const auto rq = rsrc(a.q + b * a.bsq + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldq + a.Dv) * 2);
   const auto rg = rsrc(a.dout + b * a.bsdo + hh * a.Dv, ((long long)(a.Nq - 1) * a.lddo + a.Dv) * 2);
@@ -645,15 +676,223 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
+// Cross-attention backward (Nk <= 128 keys, head dim <= 64: SDXL / SD 1.5 attn2 over the 77 text tokens), one
+// pass instead of the dQ + dK/dV pair (which recompute S and dP, stream Q / dO twice and need a query split for
+// dK/dV parallelism over one key block).  Workgroup = (query chunk, head, batch), 4 waves; wave w owns keys
+// 32w .. 32w+31: their K / V row fragments stay in registers and their dK^T / dV^T accumulators sum over the
+// chunk's queries.  The chunk is walked in rounds of 64 queries, staged by LDS-DMA (Q and dO row + transposed-read
+// images, the O row image).  A round:
+//   delta = rowsum(dO o O) of its 64 queries from the O / dO images (4 lanes per query) -> {lse, delta} table;
+//   S = Q K^T, dP = dO V^T with the key on the lane; P = exp2(S c - lse), dS = P (dP - delta) feed
+//   dV^T += dO^T P and dK^T += Q^T dS as MFMA B operands; dS^T (bf16) -> an LDS [key][query] image;
+//   dQ^T = K^T dS^T: one (32 d x 32 q) tile per wave over the active keys (stored at the next round's start).
+// 5 MFMA products per (query, key) tile instead of 7.  dK / dV: bf16 directly with one chunk, else fp32 per-chunk
+// slabs [chunk][B][Nk][H][Dv] summed in chunk order by attn_dkv_cast_kernel (deterministic).
+constexpr int XQR = 64;   // queries per round
+constexpr int XIMG = XQR * 64 * 2;                      // one [64 x 64] bf16 image
+constexpr int X_KTR = 0;                                // K transposed-read image, 128 keys (16 KiB)
+constexpr int X_QROW = 16384, X_QTR = X_QROW + XIMG, X_GROW = X_QTR + XIMG, X_GTR = X_GROW + XIMG,
+              X_OROW = X_GTR + XIMG;
+constexpr int X_DST = X_OROW + XIMG;                    // dS^T image [128 keys][64 queries] (16 KiB)
+constexpr int X_PAIRS = X_DST + 16384;                  // 64 {lse, delta}
+constexpr int X_LDS = X_PAIRS + XQR * 8;                // 72.5 KiB: two workgroups per CU
+
+__device__ __forceinline__ int cross_per(const AttnArgs& a) {
+  return ((a.Nq + a.qsplit - 1) / a.qsplit + XQR - 1) / XQR * XQR;
+}
+
+__global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int D = 64;
+  using RImg = DmaImg<D, XQR, false>;
+  using TImg = DmaImg<D, XQR, true>;
+  using KImg = DmaImg<D, 128, true>;
+  int chunk, hh, b;
+  block_ids(a, chunk, hh, b);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int nkt = (a.Nk + 31) / 32;                     // key tiles = active waves
+  const int per = cross_per(a);
+  const int qbeg = chunk * per, qend = min(a.Nq, qbeg + per);
+  const int rounds = qend > qbeg ? (qend - qbeg + XQR - 1) / XQR : 0;
+  const long long srow = ((long long)b * a.H + hh) * a.Nq;
+  const auto rq = rsrc(a.q + b * a.bsq + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldq + a.Dv) * 2);
+  const auto rg = rsrc(a.dout + b * a.bsdo + hh * a.Dv, ((long long)(a.Nq - 1) * a.lddo + a.Dv) * 2);
+  const auto ro = rsrc(a.o + b * a.bso + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldo + a.Dv) * 2);
+  const auto rk = rsrc(a.k + b * a.bsk + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldk + a.Dv) * 2);
+  RImg ri;
+  TImg ti;
+  KImg kti;
+  ri.prepare(wave, lane);
+  ti.prepare(wave, lane);
+  kti.prepare(wave, lane);
+  auto issue = [&](int q0) {   // rows >= qend (the next chunk's, or past Nq) are zero-filled
+    ri.issue(rq, smem + X_QROW, a.ldq, q0, qend, a.Dv, wave);
+    ti.issue(rq, smem + X_QTR, a.ldq, q0, qend, a.Dv, wave);
+    ri.issue(rg, smem + X_GROW, a.lddo, q0, qend, a.Dv, wave);
+    ti.issue(rg, smem + X_GTR, a.lddo, q0, qend, a.Dv, wave);
+    ri.issue(ro, smem + X_OROW, a.ldo, q0, qend, a.Dv, wave);
+  };
+  const int key0 = wave * 32;
+  kti.issue(rk, smem + X_KTR, a.ldk, 0, a.Nk, a.Dv, wave);   // rows >= Nk zero: dQ's padded keys add nothing
+  if (rounds > 0) issue(qbeg);
+  bf16x8 kf[D / 16], vf[D / 16];
+  load_row_frags<D>(kf, a.k + b * a.bsk + hh * a.Dv, a.ldk, key0, a.Nk, a.Dv);
+  load_row_frags<D>(vf, a.v + b * a.bsv + hh * a.Dv, a.ldv, key0, a.Nk, a.Dv);
+  // delta phase: thread t <-> query t >> 2 of the round, head-dim quarter t & 3
+  const int dqi = threadIdx.x >> 2, dpart = threadIdx.x & 3;
+  float lse_n = (qbeg + dqi < qend) ? a.lse[srow + qbeg + dqi] : INFINITY;   // padded queries: P = 0
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) { consume(kf[s]); consume(vf[s]); }
+  consume(lse_n);
+  const float c = a.scale * LOG2E;
+  const bool kvalid = key0 + r < a.Nk;
+
+  float16v dK[D / 32], dV[D / 32], dQ = zero16();
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) { dK[t] = zero16(); dV[t] = zero16(); }
+  const int qdt = wave & 1, qqt = wave >> 1;   // this wave's dQ tile: d tile, query tile
+  auto store_dq = [&](int q0) {
+    const int q = q0 + qqt * 32 + r;
+    bf16_t* Dp = a.dq + b * a.bsdq + (long long)min(q, a.Nq - 1) * a.lddq + hh * a.Dv;
+    store_tile_bf16(Dp, qdt * 32, dQ, a.scale, a.Dv, q < qend);
+  };
+
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int q0 = qbeg + rd * XQR;
+    wait_vmcnt<0>();   // this round's images (and the previous round's dQ stores)
+    BARRIER();
+    if (rd > 0) store_dq(q0 - XQR);
+    {   // delta of the round's queries from the LDS images (zero columns past Dv, zero rows past qend)
+      float dl = 0.f;
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        const int ch = 2 * dpart + c2;
+        const bf8 ov = *reinterpret_cast<const bf8*>(smem + X_OROW + dqi * 128 + ((ch ^ (dqi & 7)) << 4));
+        const bf8 gv = *reinterpret_cast<const bf8*>(smem + X_GROW + dqi * 128 + ((ch ^ (dqi & 7)) << 4));
+        float of[8], gf[8];
+        unpack8(ov, of);
+        unpack8(gv, gf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dl = fmaf(of[j], gf[j], dl);
+      }
+      dl += __shfl_xor(dl, 1, 64);
+      dl += __shfl_xor(dl, 2, 64);
+      if (dpart == 0) reinterpret_cast<float2*>(smem + X_PAIRS)[dqi] = make_float2(lse_n, dl);
+    }
+    BARRIER_LDS();   // the {lse, delta} table
+    if (wave < nkt) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        float16v S = zero16(), dP = zero16();
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          S = mfma32(lds_row_frag(smem + X_QROW, D * 2, qt * 32 + r, 2 * s + h), kf[s], S);
+          dP = mfma32(lds_row_frag(smem + X_GROW, D * 2, qt * 32 + r, 2 * s + h), vf[s], dP);
+        }
+        const float4* pv = reinterpret_cast<const float4*>(smem + X_PAIRS) + qt * 16;   // pairs 2j, 2j+1
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {      // registers 4g..4g+3 <-> queries qt*32 + 8g + 4h + (0..3)
+          const int q4 = 8 * g + 4 * h;
+          const float4 p01 = pv[q4 >> 1], p23 = pv[(q4 >> 1) + 1];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float4 pp = e ? p23 : p01;
+            const int i0 = 4 * g + 2 * e;
+            float p0 = __builtin_amdgcn_exp2f(fmaf(S[i0], c, -pp.x));
+            float p1 = __builtin_amdgcn_exp2f(fmaf(S[i0 + 1], c, -pp.z));
+            if (!kvalid) p0 = p1 = 0.f;    // the key is the lane: padded keys contribute nothing
+            dP[i0] = p0 * (dP[i0] - pp.y);
+            dP[i0 + 1] = p1 * (dP[i0 + 1] - pp.w);
+            S[i0] = p0;
+            S[i0 + 1] = p1;
+          }
+        }
+        const bf16x8 p0 = pack_acc(S, 0), p1 = pack_acc(S, 1), d0 = pack_acc(dP, 0), d1 = pack_acc(dP, 1);
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          dV[dt] = mfma32(tr_frag<D>(smem + X_GTR, qt * 32, 0, dt * 32), p0, dV[dt]);
+          dV[dt] = mfma32(tr_frag<D>(smem + X_GTR, qt * 32, 1, dt * 32), p1, dV[dt]);
+          dK[dt] = mfma32(tr_frag<D>(smem + X_QTR, qt * 32, 0, dt * 32), d0, dK[dt]);
+          dK[dt] = mfma32(tr_frag<D>(smem + X_QTR, qt * 32, 1, dt * 32), d1, dK[dt]);
+        }
+        // dS^T -> the [key][query] transposed-read image: registers 4g..4g+3 are 4 consecutive queries
+        const uint4 w0 = __builtin_bit_cast(uint4, d0), w1 = __builtin_bit_cast(uint4, d1);
+        char* dst = smem + X_DST;
+        const int kr = key0 + r, qc = qt * 32 + 4 * h;
+        *reinterpret_cast<uint2*>(dst + tr_off<D>(kr, qc)) = make_uint2(w0.x, w0.y);
+        *reinterpret_cast<uint2*>(dst + tr_off<D>(kr, qc + 8)) = make_uint2(w0.z, w0.w);
+        *reinterpret_cast<uint2*>(dst + tr_off<D>(kr, qc + 16)) = make_uint2(w1.x, w1.y);
+        *reinterpret_cast<uint2*>(dst + tr_off<D>(kr, qc + 24)) = make_uint2(w1.z, w1.w);
+      }
+    }
+    BARRIER_LDS();   // dS^T complete; the Q / dO / O images are free
+    if (rd + 1 < rounds) {
+      issue(q0 + XQR);
+      lse_n = (q0 + XQR + dqi < qend) ? a.lse[srow + q0 + XQR + dqi] : INFINITY;
+    }
+    dQ = zero16();
+    for (int kt = 0; kt < nkt; ++kt) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        dQ = mfma32(tr_frag<D>(smem + X_KTR, kt * 32, s, qdt * 32), tr_frag<D>(smem + X_DST, kt * 32, s, qqt * 32), dQ);
+    }
+  }
+  if (rounds > 0) store_dq(qbeg + (rounds - 1) * XQR);
+  wait_vmcnt<0>();   // no LDS-DMA may outlive the workgroup (rounds == 0: the K image)
+  if (wave >= nkt) return;
+  const int key = key0 + r;
+  if (a.qsplit > 1) {   // this chunk's fp32 slab [qsplit][B][Nk][H][Dv]; summed by attn_dkv_cast
+    if (key < a.Nk) {
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * h;
+          if (d >= a.Dv) continue;
+          const long long base = ((((long long)chunk * a.B + b) * a.Nk + key) * a.H + hh) * a.Dv + d;
+          *reinterpret_cast<float4*>(a.dk32 + base) =
+              make_float4(dK[dt][4 * g] * a.scale, dK[dt][4 * g + 1] * a.scale, dK[dt][4 * g + 2] * a.scale,
+                          dK[dt][4 * g + 3] * a.scale);
+          *reinterpret_cast<float4*>(a.dv32 + base) =
+              make_float4(dV[dt][4 * g], dV[dt][4 * g + 1], dV[dt][4 * g + 2], dV[dt][4 * g + 3]);
+        }
+    }
+  } else {
+    bf16_t* kp = a.dk + b * a.bsdk + (long long)min(key, a.Nk - 1) * a.lddk + hh * a.Dv;
+    bf16_t* vp = a.dv + b * a.bsdv + (long long)min(key, a.Nk - 1) * a.lddv + hh * a.Dv;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+      store_tile_bf16(kp, dt * 32, dK[dt], a.scale, a.Dv, key < a.Nk);
+      store_tile_bf16(vp, dt * 32, dV[dt], 1.f, a.Dv, key < a.Nk);
+    }
+  }
+}
+
 // sum the qsplit fp32 slabs [qsplit][B, Nk, H, Dv] -> bf16 dK / dV with their strides (4 elements
-// per thread; Dv % 8 == 0).  Deterministic: fixed summation order over the splits.
+// per thread; Dv % 8 == 0).  Deterministic: fixed summation order over the splits.  The split loop is
+// unrolled by 4 so each thread has 8 loads in flight (a dependent load per split made the launch latency-bound).
 __global__ void attn_dkv_cast_kernel(AttnArgs a) {
   const long long total4 = (long long)a.B * a.Nk * a.H * a.Dv / 4;
   const long long slab = total4 * 4;
   for (long long i4 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i4 < total4; i4 += (long long)gridDim.x * blockDim.x) {
     const long long i = i4 * 4;
-    float4 sk = *reinterpret_cast<const float4*>(a.dk32 + i), sv = *reinterpret_cast<const float4*>(a.dv32 + i);
-    for (int s = 1; s < a.qsplit; ++s) {
+    float4 sk = make_float4(0.f, 0.f, 0.f, 0.f), sv = sk;
+    int s = 0;
+    for (; s + 4 <= a.qsplit; s += 4) {
+      float4 k[4], v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        k[u] = *reinterpret_cast<const float4*>(a.dk32 + (s + u) * slab + i);
+        v[u] = *reinterpret_cast<const float4*>(a.dv32 + (s + u) * slab + i);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        sk.x += k[u].x; sk.y += k[u].y; sk.z += k[u].z; sk.w += k[u].w;
+        sv.x += v[u].x; sv.y += v[u].y; sv.z += v[u].z; sv.w += v[u].w;
+      }
+    }
+    for (; s < a.qsplit; ++s) {
       const float4 k = *reinterpret_cast<const float4*>(a.dk32 + s * slab + i);
       const float4 v = *reinterpret_cast<const float4*>(a.dv32 + s * slab + i);
       sk.x += k.x; sk.y += k.y; sk.z += k.z; sk.w += k.w;
@@ -674,6 +913,11 @@ __global__ void attn_dkv_cast_kernel(AttnArgs a) {
   }
 }
 
+static bool getenv_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] && v[0] != '0';
+}
+
 // the per-(batch, head) DMA descriptors address rows with 31-bit byte offsets
 static bool fits31(int rows, long long ld) { return ((long long)rows * ld + 128) * 2 < 0x7fff0000LL; }
 
@@ -686,8 +930,18 @@ static bool attn_ok(const AttnArgs& a) {
   return true;
 }
 
+// OTAMD_ATTN_XCD=0: hardware block order (the A/B reference)
+static int xcd_order() {
+  static const int on = [] {
+    const char* v = std::getenv("OTAMD_ATTN_XCD");
+    return (v && v[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
 template <typename K>
-static void launch(K kern, dim3 grid, int lds, hipStream_t s, const AttnArgs& a) {
+static void launch(K kern, dim3 grid, int lds, hipStream_t s, AttnArgs a) {
+  a.xcd = xcd_order();
   {   // LDS opt-in once per kernel instance (its LDS size is fixed by the template)
     static std::mutex mu;
     static std::unordered_set<const void*> done;
@@ -696,6 +950,23 @@ static void launch(K kern, dim3 grid, int lds, hipStream_t s, const AttnArgs& a)
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   }
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+}
+
+// one-pass cross-attention backward (attn_bwd_cross_kernel): short key sets at head dim <= 64
+// (OTAMD_ATTN_CROSS_OFF=1: the dQ + dK/dV pair for every shape, the A/B reference)
+static bool attn_cross_path(const AttnArgs& a) {
+  static const bool off = getenv_flag("OTAMD_ATTN_CROSS_OFF");
+  return a.Nk <= 128 && a.Dv <= 64 && !off;
+}
+
+// query chunks of the one-pass cross backward: ~2 workgroups per CU over (chunk, head, batch), 64-query rounds,
+// at most 16 rounds (1024 queries) per chunk; the kernel recomputes the chunk length from the count (cross_per)
+static int cross_chunks(const AttnArgs& a) {
+  const int bh = a.B * a.H;
+  const int target = std::max(1, (512 + bh - 1) / bh);
+  int per = ((a.Nq + target - 1) / target + XQR - 1) / XQR * XQR;
+  per = std::min(std::max(per, XQR), 16 * XQR);
+  return (a.Nq + per - 1) / per;
 }
 
 OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
@@ -710,6 +981,7 @@ OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
 }
 
 static int attn_qsplit(const AttnArgs& a) {
+  if (attn_cross_path(a)) return cross_chunks(a);
   const int kblocks = (a.Nk + 127) / 128;
   int qsplit = 1;
   while (kblocks * a.H * a.B * qsplit < 512 && qsplit < 64 && (a.Nq / (qsplit * 2)) >= 128) qsplit *= 2;
@@ -746,7 +1018,9 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   const int kblocks = (a.Nk + 127) / 128;
   dim3 gq((a.Nq + 127) / 128, a.H, a.B);
   dim3 gk(kblocks, a.H, a.B * qsplit);
-  if (a.Dv <= 64) {
+  if (attn_cross_path(a)) {
+    launch(attn_bwd_cross_kernel, dim3(qsplit, a.H, a.B), X_LDS, stream, a);
+  } else if (a.Dv <= 64) {
     launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
     launch(attn_bwd_dkv_kernel<64, 3>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);   // SDXL bwd 17.18 -> 16.71 ms/step
   } else {

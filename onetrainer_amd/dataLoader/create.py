@@ -49,14 +49,13 @@ def attach_cache_encoders(model, config, device) -> None:
     from ..module import vae as V
     cfg = plain(config)
     fam = _family(cfg.model_type)
-    vcfg = {"sdxl": V.sdxl_vae_config, "sd15": V.sd15_vae_config}.get(fam)
-    if vcfg is None:
-        raise NotImplementedError("latent caching for FLUX.1 needs its 16-channel VAE: cache latents offline "
-                                  "(LatentCacheWriter) and point cache_dir at them")
+    vcfg = {"sdxl": V.sdxl_vae_config, "sd15": V.sd15_vae_config, "flux": V.flux_vae_config}[fam]
     model.vae_encoder = V.AutoencoderKLEncoder(vcfg(), device, seed=0)
     model.text_encoder_1 = TE.CLIPTextEncoder(TE.clip_l_config(), device)
     if fam == "sdxl":
         model.text_encoder_2 = TE.CLIPTextEncoder(TE.clip_bigg_config(), device)
+    elif fam == "flux":
+        model.text_encoder_2 = TE.T5TextEncoder(TE.t5_xxl_config(), device)
 
 
 def _concepts(cfg) -> list:
@@ -115,6 +114,9 @@ def _tokenizers(cfg):
     toks = [CLIPTokenizer.from_pretrained(os.path.join(base, "tokenizer"))]
     if fam == "sdxl":
         toks.append(CLIPTokenizer.from_pretrained(os.path.join(base, "tokenizer_2")))
+    elif fam == "flux":
+        from transformers import AutoTokenizer   # T5TokenizerFast (tokenizer.json) or the sentencepiece T5Tokenizer
+        toks.append(AutoTokenizer.from_pretrained(os.path.join(base, "tokenizer_2")))
     return toks
 
 
@@ -132,9 +134,10 @@ def build_cache(config, model, device, rank: int = 0) -> int:
     def ids(tok, caption):
         return tok(caption, padding="max_length", max_length=77, truncation=True, return_tensors="pt").input_ids[0]
 
-    if fam == "sdxl":
-        text_fn = lambda t: TE.encode_sdxl_text(model.text_encoder_1, model.text_encoder_2,  # noqa: E731
-                                                t["tokens_1"], t["tokens_2"])
+    if fam in ("sdxl", "flux"):
+        enc_text = TE.encode_sdxl_text if fam == "sdxl" else TE.encode_flux_text
+        text_fn = lambda t: enc_text(model.text_encoder_1, model.text_encoder_2,  # noqa: E731
+                                     t["tokens_1"], t["tokens_2"])
         rows = ({"image": Image.open(p), "tokens": {"tokens_1": ids(toks[0], c), "tokens_2": ids(toks[1], c)}}
                 for p, c in samples)
     else:

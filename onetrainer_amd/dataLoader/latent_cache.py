@@ -6,7 +6,7 @@ Replaces what the reference's mgds pipeline does before and around the steps
   SampleVAEDistribution(mean) -> DiskCache -> AspectBatchSorting -> OutputPipelineModule.
 The mgds on-disk cache format is not pinned (mgds is not in this image); this build's format:
   <cache_dir>/index.json            {"version": 1, "samples": [{"file", "crop_resolution"}, ...]}
-  <cache_dir>/<i:08d>.safetensors   latent_image [h, w, 4] fp32 NHWC (VAE latent_dist.mean, unscaled),
+  <cache_dir>/<i:08d>.safetensors   latent_image [h, w, C] fp32 NHWC (VAE latent_dist.mean, unscaled; C = 4, FLUX.1 16),
                                     original_resolution / crop_offset / crop_resolution int64 [2],
                                     optional cached text states (text_encoder_*_hidden_state, pooled).
 Images are scaled / cropped on the host (data-loader work, as in mgds' worker threads), encoded on
@@ -51,7 +51,7 @@ def scale_crop(img: torch.Tensor, scale_res, crop_res, offset):
 class LatentCacheWriter:
     def __init__(self, encode_fn, cache_dir: str, bucketing, device, encode_batch: int = 8, rank: int = 0,
                  text_fn=None):
-        """encode_fn: [B, 3, H, W] fp32 [0, 1] on `device` -> latent NHWC fp32 [B, H/8, W/8, 4]
+        """encode_fn: [B, 3, H, W] fp32 [0, 1] on `device` -> latent NHWC fp32 [B, H/8, W/8, C]
         (module.vae.AutoencoderKLEncoder.encode).  text_fn (optional): {name: int64 token ids [B, T]}
         on `device` -> {cache key: [B, ...]} (module.text_encoder.encode_sdxl_text & co.), applied to
         samples that carry "tokens" -- the reference's text-encoder caching step."""

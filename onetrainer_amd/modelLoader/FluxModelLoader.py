@@ -1,14 +1,16 @@
 """FLUX.1 transformer weights from a local diffusers directory (`transformer/`, sharded or not) or an
 INTERNAL backup; the same order and failure message as modules/modelLoader/flux/FluxModelLoader.py
 (internal -> diffusers; the single-file BFL layout needs diffusers' converter and is not restated).
-LoRA: `lora/lora.safetensors` of a backup or a .safetensors file (LoRAModuleWrapper keys)."""
+LoRA: `lora/lora.safetensors` of a backup or a .safetensors file (LoRAModuleWrapper keys).
+When the trainer caches latents / text it attaches the 16-channel VAE encoder and the CLIP-L / T5-XXL encoders
+first (dataLoader/create.attach_cache_encoders); they are filled from `vae/`, `text_encoder/`, `text_encoder_2/`."""
 from __future__ import annotations
 
 import os
 import traceback
 
 from .HFModelLoaderMixin import read_diffusers_sub_module, read_single_file
-from .StableDiffusionModelLoader import load_internal_data, load_text_encoders
+from .StableDiffusionModelLoader import load_internal_data, load_text_encoders, load_vae_encoder
 
 
 def apply_flux_state_dict(transformer, sd: dict) -> None:
@@ -33,6 +35,9 @@ class FluxModelLoader:
         try:
             apply_flux_state_dict(model.transformer, read_diffusers_sub_module(base, "transformer"))
             load_text_encoders(model, base)
+            enc = getattr(model, "vae_encoder", None)
+            if enc is not None:
+                load_vae_encoder(enc, getattr(model_names, "vae_model", None) or base)
             return
         except Exception:
             stacktraces.append(traceback.format_exc())

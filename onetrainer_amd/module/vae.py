@@ -13,6 +13,9 @@ Encoder graph (forward only; nothing is trained):
   Downsample2D = F.pad(0,1,0,1) + 3x3 stride-2 conv on all but the last) | mid: ResnetBlock2D,
   single-head self-attention (GroupNorm, to_q/k/v/out with bias, residual), ResnetBlock2D |
   GN + SiLU, conv_out 512->8 | quant_conv 1x1 8->8 | mean = channels [0, 4).
+FLUX.1's AutoencoderKL (flux_vae_config, FluxBaseDataLoader.py:70-71 + BaseFluxSetup.py:229-230) has the same
+encoder with 16 latent channels (conv_out 512->32) and no quant_conv: mean = conv_out channels [0, 16); the
+setup applies (latent - shift_factor) * scaling_factor.
 Kernels: implicit-GEMM convs (stride 2 + one-sided zero padding through the conv gather's range
 check), GroupNorm(+SiLU), fused q|k|v Linear, the materialized single-head attention (512-wide
 head: batched MFMA GEMMs + row softmax), and the quant_conv mean rows as one fp32-out GEMM.
@@ -40,6 +43,8 @@ class VAEConfig:
     norm_num_groups: int = 32
     norm_eps: float = 1e-6
     scaling_factor: float = 0.13025
+    shift_factor: float = 0.0
+    use_quant_conv: bool = True
 
 
 def sdxl_vae_config() -> VAEConfig:
@@ -50,9 +55,16 @@ def sd15_vae_config() -> VAEConfig:
     return VAEConfig(scaling_factor=0.18215)
 
 
-def tiny_vae_config() -> VAEConfig:
+def flux_vae_config() -> VAEConfig:
+    """black-forest-labs/FLUX.1-dev vae/config.json: latent_channels 16, use_quant_conv false,
+    scaling_factor 0.3611, shift_factor 0.1159 (the encoder otherwise equals SDXL's)."""
+    return VAEConfig(latent_channels=16, scaling_factor=0.3611, shift_factor=0.1159, use_quant_conv=False)
+
+
+def tiny_vae_config(latent_channels: int = 4, use_quant_conv: bool = True) -> VAEConfig:
     """test size; 160 mid channels -> a 160-wide single head (materialized attention path)."""
-    return VAEConfig(block_out_channels=(64, 160), layers_per_block=1)
+    return VAEConfig(block_out_channels=(64, 160), layers_per_block=1, latent_channels=latent_channels,
+                     use_quant_conv=use_quant_conv)
 
 
 def _conv(p, cin, cout, k=3):
@@ -92,7 +104,8 @@ def vae_encoder_specs(cfg: VAEConfig):
     s += [(a + ".to_out.0.weight", (c, c), "linear", c), (a + ".to_out.0.bias", (c,), "bias", c)]
     s += _resnet("encoder.mid_block.resnets.1", c, c)
     s += _norm("encoder.conv_norm_out", c) + _conv("encoder.conv_out", c, 2 * cfg.latent_channels)
-    s += _conv("quant_conv", 2 * cfg.latent_channels, 2 * cfg.latent_channels, 1)
+    if cfg.use_quant_conv:
+        s += _conv("quant_conv", 2 * cfg.latent_channels, 2 * cfg.latent_channels, 1)
     return s
 
 
@@ -122,7 +135,7 @@ def flops_per_image(cfg: VAEConfig, h: int, w: int) -> float:
     c = ch[-1]
     macs += 2 * (2 * hw * c * c * 9) + 4 * hw * c * c + 2 * hw * hw * c
     lc = 2 * cfg.latent_channels
-    macs += hw * c * lc * 9 + hw * lc * lc
+    macs += hw * c * lc * 9 + (hw * lc * lc if cfg.use_quant_conv else 0)
     return 2.0 * macs
 
 
@@ -135,7 +148,7 @@ class AutoencoderKLEncoder:
         self.specs = vae_encoder_specs(cfg)
         self.store = FlatParamStore([(n, _store_shape(n, sh, k), "vae") for n, sh, k, _ in self.specs], dtype,
                                     self.device, trainable=False)
-        self.config = {"scaling_factor": cfg.scaling_factor}
+        self.config = {"scaling_factor": cfg.scaling_factor, "shift_factor": cfg.shift_factor}
         if seed is not None:
             self.init_weights(seed)
 
@@ -174,7 +187,8 @@ class AutoencoderKLEncoder:
         return out
 
     def load_state_dict(self, sd):
-        """diffusers AutoencoderKL keys (encoder.* and quant_conv.*; decoder keys are ignored)."""
+        """diffusers AutoencoderKL keys (encoder.* and quant_conv.* when the config has one; decoder keys are
+        ignored)."""
         with torch.no_grad():
             for name, shape, kind, _ in self.specs:
                 if tuple(sd[name].shape) != tuple(shape):
@@ -215,7 +229,7 @@ class AutoencoderKLEncoder:
     # ----- encode -------------------------------------------------------------------------------
     @torch.no_grad()
     def encode_nhwc(self, x):
-        """x: [B, H, W, 8] bf16 in [-1, 1] (channels >= 3 zero) -> latent mean [B, H/8, W/8, 4] fp32."""
+        """x: [B, H, W, 8] bf16 in [-1, 1] (channels >= 3 zero) -> latent mean [B, H/8, W/8, L] fp32."""
         cfg = self.cfg
         ch = cfg.block_out_channels
         K._req(x.shape[1] % (1 << (len(ch) - 1)) == 0 and x.shape[2] % (1 << (len(ch) - 1)) == 0,
@@ -233,9 +247,14 @@ class AutoencoderKLEncoder:
         h = self._attention(h, "encoder.mid_block.attentions.0")
         h = self._resnet(h, "encoder.mid_block.resnets.1")
         h = self._gn(h, "encoder.conv_norm_out", True)
+        L = cfg.latent_channels
+        if not cfg.use_quant_conv:
+            # DiagonalGaussianDistribution(conv_out(h)).mean: only conv_out's first L output channels (the stored
+            # weight's first L rows), in the reference's autocast dtype
+            mean = K.conv2d(h, self.W("encoder.conv_out.weight")[:L], bias=self.W("encoder.conv_out.bias")[:L])
+            return mean.float()
         h = K.conv2d(h, self.W("encoder.conv_out.weight"), bias=self.W("encoder.conv_out.bias"))
         N, H, W_, C2 = h.shape
-        L = cfg.latent_channels
         # DiagonalGaussianDistribution(quant_conv(h)).mean: only the first L quant_conv rows
         mean = K.linear(h.view(-1, C2), self.W("quant_conv.weight")[:L], bias=self.W("quant_conv.bias")[:L],
                         out_dtype=torch.float32)

@@ -106,6 +106,13 @@ def test_vae_encoder_spec_and_flops():
     om = OV.AutoencoderKLEncoder(cfg)
     assert {n for n, *_ in specs} == set(om.state_dict())
     assert sum(math.prod(s) for _, s, _, _ in specs) == sum(p.numel() for p in om.parameters()) == 34_163_664
+    # FLUX.1's encoder: 16 latent channels (conv_out 512 -> 32), no quant_conv
+    fcfg = V.flux_vae_config()
+    fspecs = V.vae_encoder_specs(fcfg)
+    fom = OV.AutoencoderKLEncoder(fcfg)
+    assert {n for n, *_ in fspecs} == set(fom.state_dict()) and not any(n.startswith("quant_conv") for n, *_ in fspecs)
+    n_flux = 34_163_664 - (8 * 8 + 8) - (512 * 8 * 9 + 8) + (512 * 32 * 9 + 32)
+    assert sum(math.prod(s) for _, s, _, _ in fspecs) == sum(p.numel() for p in fom.parameters()) == n_flux
 
 
 def test_flux_spec_and_flops():

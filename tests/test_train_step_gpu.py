@@ -187,3 +187,30 @@ def test_step_graph_matches_eager(dev, monkeypatch):
     assert torch.equal(l0, l1), (l0, l1)
     assert torch.equal(p0, p1)
     assert torch.equal(s0, s1)
+
+
+def test_full_sdxl_steps_bitwise_repeatable(dev):
+    """The step is deterministic under its real concurrency (weight-gradient stream, split-K slabs, the one-pass
+    cross-attention backward's LDS hand-offs, the optimizer's overlapped chunks): the full SDXL UNet at 512^2 b=2,
+    three steps from the same seed, run twice, gives bit-identical parameters, moments and losses.  A missing
+    LDS-write fence before a barrier showed up exactly here (run-to-run loss drift), not in the per-kernel tests."""
+    def run():
+        cfg = TrainConfig.default_values()
+        cfg.batch_size = 2
+        cfg.learning_rate = 1e-4
+        cfg.learning_rate_warmup_steps = 0
+        tr = GenericTrainer(cfg, seed=0)
+        tr.start()
+        batch = synthetic_sdxl_batch(2, 512, 512, dev, seed=1)
+        losses = [tr.train_step(batch).float() for _ in range(3)]
+        st = tr.model.train_store
+        st.wait_params()
+        torch.cuda.synchronize()
+        out = (torch.stack(losses).cpu(), st.data.clone(), tr.model.optimizer.exp_avg.clone())
+        del tr
+        torch.cuda.empty_cache()
+        return out
+
+    a, b = run(), run()
+    assert torch.equal(a[0], b[0]), (a[0], b[0])
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])

@@ -17,10 +17,13 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
-@pytest.mark.parametrize("cfgname,B,H,W", [("tiny", 2, 64, 96), ("sdxl", 1, 256, 256)])
+@pytest.mark.parametrize("cfgname,B,H,W", [("tiny", 2, 64, 96), ("sdxl", 1, 256, 256), ("tiny16", 2, 64, 96),
+                                          ("flux", 1, 256, 256)])
 def test_vae_encode_matches_oracle(dev, cfgname, B, H, W):
+    """SDXL / SD 1.5 (4 latent channels + quant_conv) and FLUX.1 (16 latent channels, no quant_conv)"""
     torch.manual_seed(0)
-    cfg = V.tiny_vae_config() if cfgname == "tiny" else V.sdxl_vae_config()
+    cfg = {"tiny": V.tiny_vae_config, "sdxl": V.sdxl_vae_config, "flux": V.flux_vae_config,
+           "tiny16": lambda: V.tiny_vae_config(16, False)}[cfgname]()
     enc = V.AutoencoderKLEncoder(cfg, dev, seed=1)
     om = OV.AutoencoderKLEncoder(cfg)
     om.load_state_dict({k: v.float().cpu() for k, v in enc.state_dict().items()})
@@ -30,7 +33,7 @@ def test_vae_encode_matches_oracle(dev, cfgname, B, H, W):
                          cfg.latent_channels) and lat.dtype == torch.float32
     with torch.no_grad():
         # the oracle sees the same bf16-rounded rescaled input
-        ref = om.quant_conv(om.encoder(((img * 2 - 1).bfloat16().float())))[:, :cfg.latent_channels]
+        ref = om.moments((img * 2 - 1).bfloat16().float())[:, :cfg.latent_channels]
     ref = ref.permute(0, 2, 3, 1)
     err = (lat.cpu() - ref).abs().max() / ref.abs().max()
     assert err < 3e-2, f"rel err {err}"
@@ -87,3 +90,41 @@ def test_cache_then_train_on_buckets(dev, tmp_path):
         assert torch.isfinite(loss).item()
         shapes_seen.add(tuple(batch["latent_image"].shape))
     assert len(shapes_seen) >= 2
+
+
+def test_flux_cache_then_train(dev, tmp_path):
+    """C5's latent caching (FluxBaseDataLoader.py:70-71): images -> the 16-channel FLUX VAE encoder (no quant_conv)
+    -> latent cache (16 channels) -> reader -> FLUX.1 LoRA train steps, whose prologue applies
+    (latent - shift_factor) * scaling_factor (BaseFluxSetup.py:229-230)."""
+    from onetrainer_amd.dataLoader.aspect_bucketing import AspectBucketing
+    from onetrainer_amd.dataLoader.latent_cache import LatentCacheDataLoader, LatentCacheWriter
+    from onetrainer_amd.module import flux as FX
+    from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
+    from onetrainer_amd.util import create
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+    torch.manual_seed(0)
+    enc = V.AutoencoderKLEncoder(V.tiny_vae_config(16, False), dev, seed=1)
+    fcfg = FX.tiny_flux_config()
+    ab = AspectBucketing(128, 64)
+    shapes = [(128, 128), (120, 130), (128, 128), (130, 120)]
+    samples = [{"image": torch.rand(3, h, w),
+                "text": {"text_encoder_1_pooled_state": torch.randn(fcfg.pooled_projection_dim).bfloat16(),
+                         "text_encoder_2_hidden_state": torch.randn(77, fcfg.joint_attention_dim).bfloat16()}}
+               for h, w in shapes]
+    LatentCacheWriter(lambda im: enc.encode(im), str(tmp_path), ab, dev, encode_batch=2).write(samples)
+    cfg = TrainConfig.default_values()
+    cfg.model_type, cfg.training_method, cfg.timestep_distribution = "FLUX_DEV_1", "LORA", "LOGIT_NORMAL"
+    cfg.batch_size = 2
+    cfg.learning_rate_warmup_steps = 0
+    model = create.create_model(cfg, dev, seed=3, flux_config=fcfg)
+    dl = LatentCacheDataLoader(str(tmp_path), batch_size=2, device=dev, seed=0)
+    tr = GenericTrainer(cfg, model=model, data_loader=dl)
+    tr.start()
+    dl.get_data_set().start_next_epoch()
+    n = 0
+    for batch in dl.get_data_loader():
+        assert batch["latent_image"].shape[1] == 16
+        loss = tr.train_step(batch)
+        assert torch.isfinite(loss).item()
+        n += 1
+    assert n >= 1

@@ -51,6 +51,7 @@ def main():
     torch.cuda.synchronize()
 
     recs = []
+    main_handle = torch.cuda.current_stream().cuda_stream
     K._HOST["off"] = True   # launch through the ctypes path, whose _gemm is wrapped below
     orig = K._gemm
 
@@ -62,7 +63,8 @@ def main():
         e0.record()
         orig(a, splits, device)
         e1.record()
-        key = (MODES[a.amode], MODES[a.bmode], a.M, a.N, a.K, tile, s_out.value)
+        side = torch.cuda.current_stream().cuda_stream != main_handle
+        key = (MODES[a.amode], MODES[a.bmode], a.M, a.N, a.K, tile, s_out.value, "side" if side else "main")
         recs.append((key, e0, e1))
 
     K._gemm = timed
@@ -76,11 +78,11 @@ def main():
         agg[key][1] += e0.elapsed_time(e1)
     total = 0.0
     for key, (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        am, bm, M, N, Kd, tile, sp = key
+        am, bm, M, N, Kd, tile, sp, st = key
         per = ms / args.steps
         total += per
         us = ms / n * 1e3
-        print(json.dumps({"a": am, "b": bm, "M": M, "N": N, "K": Kd, "tile": tile, "splits": sp,
+        print(json.dumps({"stream": st, "a": am, "b": bm, "M": M, "N": N, "K": Kd, "tile": tile, "splits": sp,
                           "calls_per_step": n / args.steps, "ms_per_step": round(per, 3), "us": round(us, 1),
                           "tflops": round(2.0 * M * N * Kd / (us * 1e-6) / 1e12, 1)}), flush=True)
     print(json.dumps({"total_ms_per_step": round(total, 2), "launches_per_step": len(recs) / args.steps}))
