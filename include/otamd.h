@@ -125,7 +125,8 @@ int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream);
 /* replaces: autograd of scaled_dot_product_attention (GenericTrainer.py:693-696) */
 int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream);
 
-/* workspace bytes otamd_attn_bwd needs for these arguments ({lse, delta} pairs + split-query partials) */
+/* workspace bytes otamd_attn_bwd needs for these arguments (16-byte bias records per query + split-query or
+   per-chunk dK/dV partials) */
 long long otamd_attn_bwd_ws_bytes(const AttnArgs* in);
 
 /* replaces: ABI check */

@@ -132,6 +132,15 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int row0, int s, int 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// x ~= t0 + t1 + t2 (bf16 each, round-to-nearest at every stage): returns {t0 | t1 << 16, t2}
+__device__ __forceinline__ uint2 split3_bf16(float x) {
+  const bf16_t t0 = f2bf(x);
+  const float r1 = x - bf2f(t0);
+  const bf16_t t1 = f2bf(r1);
+  const bf16_t t2 = f2bf(r1 - bf2f(t1));
+  return make_uint2((uint32_t)t0 | ((uint32_t)t1 << 16), (uint32_t)t2);
+}
+
 __device__ __forceinline__ bf16x8 pack_acc(const float16v& a, int s) {
   bf16x8 r;
 #pragma unroll
@@ -449,7 +458,15 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
     lse2 = a.lse[srow + q];
   }
   dlt += __shfl_xor(dlt, 32, 64);
-  if (h == 0 && q < a.Nq) reinterpret_cast<float2*>(const_cast<float*>(a.delta))[srow + q] = make_float2(lse2, dlt);
+  // the dK/dV kernel's bias record of this query: -lse / c and -delta, each as three bf16 terms (hi + mid + lo
+  // carry ~24 bits), [b0 b1 b2 d0 d1 d2 0 0]: used there as an MFMA A-operand k-step so S' = S - lse/c and
+  // dP' = dP - delta come out of the accumulator chains (attn_bwd_dkv_kernel)
+  if (h == 0 && q < a.Nq) {
+    const float cc = a.scale * LOG2E;
+    const uint2 bl = split3_bf16(-lse2 / cc), dl = split3_bf16(-dlt);
+    reinterpret_cast<uint4*>(const_cast<float*>(a.delta))[srow + q] =
+        make_uint4(bl.x, bl.y | (dl.x << 16), (dl.x >> 16) | (dl.y << 16), 0u);
+  }
   consume(dlt);
   consume(lse2);
 #pragma unroll
@@ -511,18 +528,24 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 }
 
 // dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of 32 in this split's range.
-// Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 {lse, delta} pairs.
+// Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 bias records (written by the dQ
+// kernel: -lse/c and -delta as three bf16 terms each).  The record is one extra MFMA k-step of S and of dP
+// (A = the record of the lane's query, B = ones in the matching three k slots), so the accumulators come out as
+// S - lse/c and dP - delta: no per-score subtraction and no per-register {lse, delta} reads in the softmax.
 // D = 128: the dK/dV accumulators alone take 128 VGPRs and the 3-deep ring (99 KiB) already limits a
 // CU to one block, so the full 512-entry register file is used instead of spilling at 256.
 // (A software-pipelined D = 128 variant -- S / dP of tile t+1 on the MFMA pipe during tile t's
 // softmax, 4-deep ring -- measured slower: 1487-1510 vs 1349 us for the Flux bwd; not kept.)
 // OCC = waves per SIMD.  D = 64 at OCC = 3 (<= 168 VGPRs: the tile loop not unrolled) fits 768 blocks on
 // the chip, the SDXL level-2 grid (8 key blocks x 20 heads x 4 = 640) in one round instead of 1.25 at OCC 2.
+template <int D> constexpr int dkv_stage() { return 4 * QT * D * 2 + QT * 16; }
+template <int D> constexpr int dkv_lds() { return 3 * dkv_stage<D>(); }   // the kernel's 3-deep ring
+
 template <int D, int OCC = 1>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = QT * D * 2;                 // one [32 x D] image
-  constexpr int STG = 4 * TB + QT * 8;           // + 32 float2 pairs
+  constexpr int STG = dkv_stage<D>();            // 4 images + 32 16-byte bias records
   constexpr int NS = 3;                          // 50 KiB (D = 64): 3 blocks per CU
   using RImg = DmaImg<D, QT, false>;
   using TImg = DmaImg<D, QT, true>;
@@ -536,7 +559,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   const long long srow = ((long long)b * a.H + hh) * a.Nq;
   const auto rq = rsrc(a.q + b * a.bsq + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldq + a.Dv) * 2);
   const auto rg = rsrc(a.dout + b * a.bsdo + hh * a.Dv, ((long long)(a.Nq - 1) * a.lddo + a.Dv) * 2);
-  const auto rp = rsrc(a.delta + 2 * srow, (long long)a.Nq * 8);
+  const auto rp = rsrc(a.delta + 4 * srow, (long long)a.Nq * 16);
   RImg ri;
   TImg ti;
   ri.prepare(wave, lane);
@@ -552,9 +575,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
     ti.issue(rq, st + TB, a.ldq, qt0, qend, a.Dv, wave);
     ri.issue(rg, st + 2 * TB, a.lddo, qt0, qend, a.Dv, wave);
     ti.issue(rg, st + 3 * TB, a.lddo, qt0, qend, a.Dv, wave);
-    if ((lane >> 4) == wave) {   // 64 floats = 32 pairs; wave w moves floats 16w .. 16w+15
-      const unsigned off = (qt0 + (lane >> 1) < qend) ? (unsigned)(2 * qt0 + lane) * 4u : OFF_INVALID;
-      dma4(rp, st + 4 * TB, off);
+    if (lane < 8) {   // 32 records of 16 B; wave w moves records 8w .. 8w+7
+      const int qr = qt0 + 8 * wave + lane;
+      const unsigned off = qr < qend ? (unsigned)qr * 16u : OFF_INVALID;
+      dma16(rp, st + 4 * TB + 128 * wave, off);
     }
   };
 
@@ -572,46 +596,47 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) { dK[t] = zero16(); dV[t] = zero16(); }
 
-  // S = Q K^T and dP = dO V^T of one query tile (key on the lane)
+  // the bias k-step's B operands: ones in k slots 0..2 (S) / 3..5 (dP) of the lower lane half, zero elsewhere
+  bf16x8 ones_s, ones_d;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ones_s[j] = (__bf16)((h == 0 && j < 3) ? 1.f : 0.f);
+    ones_d[j] = (__bf16)((h == 0 && j >= 3 && j < 6) ? 1.f : 0.f);
+  }
+  // S' = Q K^T - lse/c and dP' = dO V^T - delta of one query tile (key on the lane)
   auto sdp = [&](float16v& S_, float16v& dP_, const char* st) {
-    S_ = zero16();
-    dP_ = zero16();
+    const bf16x8 rec = *reinterpret_cast<const bf16x8*>(st + 4 * TB + r * 16);   // this lane's query
+    S_ = mfma32(rec, ones_s, zero16());
+    dP_ = mfma32(rec, ones_d, zero16());
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       S_ = mfma32(lds_row_frag(st, D * 2, r, 2 * s + h), kf[s], S_);
       dP_ = mfma32(lds_row_frag(st + 2 * TB, D * 2, r, 2 * s + h), vf[s], dP_);
     }
   };
-  // P = exp2(S c - lse), dS = P (dP - delta), packed as the dV / dK B operands
+  // P = exp2(S' c), dS = P dP', packed as the dV / dK B operands
   auto softmax_pack = [&](float16v& S, float16v& dP, const char* st, bf16x8 (&pk)[4]) {
-    const float4* pv = reinterpret_cast<const float4*>(st + 4 * TB);   // pv[j] = pairs 2j, 2j+1
+    (void)st;
+    if constexpr (D == 64) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {      // registers 4g..4g+3 <-> queries 8g + 4h + (0..3)
-      const int q4 = 8 * g + 4 * h;
-      const float4 p01 = pv[q4 >> 1], p23 = pv[(q4 >> 1) + 1];   // {lse,dl} of q4, q4+1 | q4+2, q4+3
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(S[i] * c);
+        dP[i] = p * dP[i];
+        S[i] = p;
+      }
+    } else {   // packed (see exp2_scaled_pk)
+      const f2v c2 = {c, c};
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const float4 pp = e ? p23 : p01;
-        const int i0 = 4 * g + 2 * e;
-        if constexpr (D == 64) {
-          const float p0 = __builtin_amdgcn_exp2f(fmaf(S[i0], c, -pp.x));
-          const float p1 = __builtin_amdgcn_exp2f(fmaf(S[i0 + 1], c, -pp.z));
-          dP[i0] = p0 * (dP[i0] - pp.y);
-          dP[i0 + 1] = p1 * (dP[i0 + 1] - pp.w);
-          S[i0] = p0;
-          S[i0 + 1] = p1;
-        } else {   // packed (see exp2_scaled_pk)
-          f2v x = {S[i0], S[i0 + 1]};
-          const f2v ls = {pp.x, pp.z}, dl = {pp.y, pp.w}, c2 = {c, c};
-          x = x * c2 - ls;
-          const f2v p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-          f2v d = {dP[i0], dP[i0 + 1]};
-          d = p * (d - dl);
-          S[i0] = p.x;
-          S[i0 + 1] = p.y;
-          dP[i0] = d.x;
-          dP[i0 + 1] = d.y;
-        }
+      for (int k = 0; k < 8; ++k) {
+        f2v x = {S[2 * k], S[2 * k + 1]};
+        x = x * c2;
+        const f2v p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+        f2v d = {dP[2 * k], dP[2 * k + 1]};
+        d = p * d;
+        S[2 * k] = p.x;
+        S[2 * k + 1] = p.y;
+        dP[2 * k] = d.x;
+        dP[2 * k + 1] = d.y;
       }
     }
     pk[0] = pack_acc(S, 0);
@@ -980,22 +1005,25 @@ OTAMD_API int otamd_attn_fwd(const AttnArgs* in, hipStream_t stream) {
   return OTAMD_OK;
 }
 
-static int attn_qsplit(const AttnArgs& a) {
-  if (attn_cross_path(a)) return cross_chunks(a);
+// dK/dV query split of the dQ + dK/dV pair (cross = false) or the chunk count of the one-pass cross kernel
+static int attn_qsplit(const AttnArgs& a, bool cross) {
+  if (cross) return cross_chunks(a);
   const int kblocks = (a.Nk + 127) / 128;
   int qsplit = 1;
   while (kblocks * a.H * a.B * qsplit < 512 && qsplit < 64 && (a.Nq / (qsplit * 2)) >= 128) qsplit *= 2;
   return qsplit;
 }
 
-// workspace bytes otamd_attn_bwd needs: {lse, delta} pairs + (split queries) fp32 dK/dV partials
-OTAMD_API long long otamd_attn_bwd_ws_bytes(const AttnArgs* in) {
+static long long attn_ws_bytes(const AttnArgs* in, bool cross) {
   if (!in || in->B <= 0 || in->H <= 0 || in->Nq <= 0 || in->Nk <= 0 || in->Dv <= 0) return -1;
   const long long nrow = (long long)in->B * in->H * in->Nq;
   const long long nkv = (long long)in->B * in->Nk * in->H * in->Dv;
-  const int qs = attn_qsplit(*in);
-  return nrow * 8 + 256 + (qs > 1 ? 2LL * qs * nkv * 4 : 0);
+  const int qs = attn_qsplit(*in, cross);
+  return nrow * 16 + 256 + (qs > 1 ? 2LL * qs * nkv * 4 : 0);
 }
+
+// workspace bytes otamd_attn_bwd needs: 16-byte bias records per query + (split queries) fp32 dK/dV partials
+OTAMD_API long long otamd_attn_bwd_ws_bytes(const AttnArgs* in) { return in ? attn_ws_bytes(in, attn_cross_path(*in)) : -1; }
 
 // ws: otamd_attn_bwd_ws_bytes(args) bytes, 16-byte aligned; lse from the forward
 OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream) {
@@ -1005,27 +1033,28 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
       (((uintptr_t)ws | (uintptr_t)a.dq | (uintptr_t)a.dk | (uintptr_t)a.dv) & 15))
     return OTAMD_EINVAL;   // 16-byte row stores
   if (((uintptr_t)a.dout & 15) || !fits31(a.Nq, a.lddo)) return OTAMD_EINVAL;
+  const bool cross = attn_cross_path(a);
   const long long nrow = (long long)a.B * a.H * a.Nq;
   const long long nkv = (long long)a.B * a.Nk * a.H * a.Dv;
-  const int qsplit = attn_qsplit(a);
+  const int qsplit = attn_qsplit(a, cross);
   a.qsplit = qsplit;
-  if (ws_bytes < otamd_attn_bwd_ws_bytes(in)) return OTAMD_EINVAL;
-  a.delta = ws;   // {lse, delta} pairs: written by the dQ kernel, read by dK/dV
+  if (ws_bytes < attn_ws_bytes(in, cross)) return OTAMD_EINVAL;
+  a.delta = ws;   // bias records: written by the dQ kernel, read by dK/dV
   if (qsplit > 1) {   // every slab element is written by exactly one block: no memset
-    a.dk32 = ws + ((nrow * 2 + 64) / 64) * 64;
+    a.dk32 = ws + ((nrow * 4 + 64) / 64) * 64;
     a.dv32 = a.dk32 + (long long)qsplit * nkv;
   }
   const int kblocks = (a.Nk + 127) / 128;
   dim3 gq((a.Nq + 127) / 128, a.H, a.B);
   dim3 gk(kblocks, a.H, a.B * qsplit);
-  if (attn_cross_path(a)) {
+  if (cross) {
     launch(attn_bwd_cross_kernel, dim3(qsplit, a.H, a.B), X_LDS, stream, a);
   } else if (a.Dv <= 64) {
     launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
-    launch(attn_bwd_dkv_kernel<64, 3>, gk, 3 * (4 * QT * 64 * 2 + QT * 8), stream, a);   // SDXL bwd 17.18 -> 16.71 ms/step
+    launch(attn_bwd_dkv_kernel<64, 3>, gk, dkv_lds<64>(), stream, a);   // SDXL bwd 17.18 -> 16.71 ms/step
   } else {
-    launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // bwd 1349 vs 1467 us (64-key tiles)
-    launch(attn_bwd_dkv_kernel<128>, gk, 3 * (4 * QT * 128 * 2 + QT * 8), stream, a);
+    launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // 1349 vs 1467 us (64-key tiles)
+    launch(attn_bwd_dkv_kernel<128>, gk, dkv_lds<128>(), stream, a);
   }
   OTAMD_CHECK_LAUNCH();
   if (qsplit > 1) {

@@ -7,6 +7,8 @@ modules/dataLoader/StableDiffusionXLBaseDataLoader.py:65-100 (RescaleImageChanne
 diffusers@5873377 and mgds@11ff4aa are not in this image; the graph is restated from the ddconfig
 the reference pins in resources/model_config/stable_diffusion_xl/sd_xl_base.yaml (ch 128,
 ch_mult [1,2,4,4], num_res_blocks 2, z_channels 4, double_z, attn only in the mid block).
+FLUX.1 (FluxBaseDataLoader.py:70-71): 16 latent channels and no quant_conv (cfg.use_quant_conv False): the
+mean is conv_out's first 16 channels.
 PARITY UNPINNED: no reference test or fixture pins the VAE numerics.
 """
 from __future__ import annotations
@@ -118,9 +120,14 @@ class AutoencoderKLEncoder(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.encoder = Encoder(cfg)
-        self.quant_conv = nn.Conv2d(2 * cfg.latent_channels, 2 * cfg.latent_channels, 1)
+        q = getattr(cfg, "use_quant_conv", True)
+        self.quant_conv = nn.Conv2d(2 * cfg.latent_channels, 2 * cfg.latent_channels, 1) if q else None
+
+    def moments(self, x):
+        """x: rescaled image in [-1, 1] -> the DiagonalGaussianDistribution parameters"""
+        h = self.encoder(x)
+        return self.quant_conv(h) if self.quant_conv is not None else h
 
     def forward(self, images01):
         """images in [0, 1] NCHW -> latent_dist.mean NCHW (RescaleImageChannels + encode + mean)."""
-        moments = self.quant_conv(self.encoder(images01 * 2.0 - 1.0))
-        return moments[:, :self.cfg.latent_channels]
+        return self.moments(images01 * 2.0 - 1.0)[:, :self.cfg.latent_channels]

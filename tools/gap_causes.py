@@ -29,11 +29,25 @@ def main():
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     kc, rc = cols(c, "kernels"), cols(c, "regions")
-    key = next((k for k in ("correlation_id", "corr_id", "stack_id", "event_id") if k in kc and k in rc), None)
+    # the column linking a dispatch to its launch call differs between rocpd versions: take the candidate whose
+    # kernels start shortly after their launch call (median lag between 0 and 100 ms)
+    key, best = None, None
+    for k in ("corr_id", "stack_id", "event_id", "correlation_id"):
+        if k not in kc or k not in rc:
+            continue
+        ls = dict(c.execute(f"select {k}, start from regions where name like '%aunch%'").fetchall())
+        lag = sorted(ks - ls[i] for i, ks in c.execute(f"select {k}, start from kernels").fetchall() if i in ls)
+        if not lag:
+            continue
+        med = lag[len(lag) // 2] / 1e6
+        print(f"candidate {k}: {len(lag)} matched, median kernel-after-launch lag {med:.3f} ms")
+        if 0 <= med < 100 and (best is None or len(lag) > best):
+            key, best = k, len(lag)
     if key is None:
         print("kernels columns:", kc)
         print("regions columns:", rc)
-        raise SystemExit("no common correlation column")
+        raise SystemExit("no plausible correlation column")
+    print(f"join column: {key}; kernels columns: {kc}; regions columns: {rc}")
     ks = c.execute(f"select name, stream_id, start, end, {key} from kernels order by start").fetchall()
     marks = [r[2] for r in ks if a.marker in r[0]]
     t0, t1 = marks[-4], marks[-3]     # the last timed step (bench.py runs two roofline steps after it)
@@ -46,6 +60,12 @@ def main():
         elif name.startswith(("hipMalloc", "hipFree", "hipExtMalloc")):
             if t0 - 1e9 < s < t1:
                 allocs.append((s, e, name))
+    lags = sorted((r[2] - launch[r[4]][0]) / 1e3 for r in step if r[4] in launch)
+    if lags:
+        print(f"kernel start - launch call start (us): n {len(lags)}, min {lags[0]:.1f}, median {lags[len(lags) // 2]:.1f}, "
+              f"max {lags[-1]:.1f}; kernels without a launch record: {sum(1 for r in step if r[4] not in launch)}")
+    names = collections.Counter(n for n, *_ in c.execute("select name from regions").fetchall())
+    print("region names:", names.most_common(12))
     by = collections.defaultdict(list)
     for r in step:
         by[r[1]].append(r)
