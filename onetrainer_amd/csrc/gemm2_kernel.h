@@ -16,6 +16,13 @@
 #pragma once
 #include "gemm.h"
 
+// Timing ablations of the K loop (tools/gemm_ablate.sh builds them as separate libraries; results are garbage):
+//   1 = no DMA after the prologue, 2 = no MFMA (fragments kept live), 3 = no fragment reads after the prologue,
+//   4 = no barrier in the loop.  0 (default): the real kernel.
+#ifndef OTAMD_GEMM_ABL
+#define OTAMD_GEMM_ABL 0
+#endif
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) short4v lds_s4_t;
 #define OFF_INVALID 0x80000000u
@@ -284,6 +291,13 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     for (int j = 0; j < NJ; ++j) f[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 32 * h) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 32 * h);
   };
   auto mfma_block = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ]) {
+    if constexpr (OTAMD_GEMM_ABL == 2) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(fb[j]));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -349,6 +363,12 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     BARRIER();
     load_b(fb0, smem + ABYTES, 0);
     load_a(fa0, smem, 0);
+    if constexpr (OTAMD_GEMM_ABL == 3) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa1[i] = fa0[i];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb1[j] = fb0[j];
+    }
   }
   // ---- column sums of A (CS) ----
   static_assert(!CS || (AM == OPM_MN && !SEG2), "column sums of an MN-mode A, single segment");
@@ -405,16 +425,18 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     const int nstg = stg + 1 == NS ? 0 : stg + 1;
     // phase A
     __builtin_amdgcn_sched_barrier(0);
-    load_b(fb1, ib, 1);
-    load_a(fa1, ia, 1);
+    if constexpr (OTAMD_GEMM_ABL != 3) {
+      load_b(fb1, ib, 1);
+      load_a(fa1, ia, 1);
+    }
     mfma_block(fa0, fb0);
-    interleave();
+    if constexpr (OTAMD_GEMM_ABL != 3) interleave();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // tile kt+1 has landed: the tiles after it that may still be in flight are kt+2 .. min(kt+NS-1, nk-1)
     wait_tiles(min(NS - 2, nk - kt - 2));
-    BARRIER();
-    if (kt + NS < nk) issue_tile(smem + stg * STAGE, kbeg + (kt + NS) * 64);   // refill tile kt's slot
+    if constexpr (OTAMD_GEMM_ABL != 4) BARRIER();
+    if (OTAMD_GEMM_ABL != 1 && kt + NS < nk) issue_tile(smem + stg * STAGE, kbeg + (kt + NS) * 64);   // refill tile kt's slot
     if constexpr (CS) {   // tile kt+1: published by this barrier, refilled only after the next one
       __builtin_amdgcn_sched_barrier(0);
       if (cs_on && kt + 1 < nk) colsum_tile(smem + nstg * STAGE);
@@ -423,10 +445,12 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     __builtin_amdgcn_sched_barrier(0);
     {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
       const char* na = smem + nstg * STAGE;
-      load_b(fb0, na + ABYTES, 0);
-      load_a(fa0, na, 0);
+      if constexpr (OTAMD_GEMM_ABL != 3) {
+        load_b(fb0, na + ABYTES, 0);
+        load_a(fa0, na, 0);
+      }
       mfma_block(fa1, fb1);
-      interleave();
+      if constexpr (OTAMD_GEMM_ABL != 3) interleave();
     }
     __builtin_amdgcn_sched_barrier(0);
     stg = nstg;

@@ -37,7 +37,7 @@ def timeit(fn, n=20):
 dev = torch.device("cuda:0")
 M = int(os.environ.get("KSCAN_M", os.environ.get("KSCAN_MN", "4096")))
 N = int(os.environ.get("KSCAN_N", os.environ.get("KSCAN_MN", "4096")))
-for k in (256, 640, 1280, 2560, 5120, 10240):
+for k in (64, 128, 256, 640, 1280, 2560, 5120, 10240):
     x = torch.randn(M, k, device=dev).bfloat16()
     w = torch.randn(N, k, device=dev).bfloat16()
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
