@@ -43,7 +43,6 @@ struct AttnArgs {
 };
 
 #define KT 64   // keys per staged tile (fwd / dQ)
-#define QT 32   // queries per staged tile (dK/dV)
 #define OFF_INVALID 0x80000000u
 static constexpr float LOG2E = 1.4426950408889634f;
 
@@ -132,6 +131,50 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int row0, int s, int 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Dual-use image (cdna_hip_programming.md T10, "one image for row reads AND transposed reads"): [rows][D] bf16,
+// 16-byte chunk ch of row r stored at chunk ch ^ dsw(r).  One copy of a tile serves the ds_read_b128 row reads of a
+// 32x32x16 operand (lds_row_frag's pattern) and the ds_read_b64_tr_b16 reads (tr_frag's pattern), both
+// conflict-free under the gfx950 bank rule (64 x 4-byte banks; b128 in four 16-lane groups, tr_b16 in two 32-lane
+// halves: tools/lds_bank_model.py enumerates every XOR of the row bits and prints the cost of each read).  The
+// row-only swizzle above (chunk ^ (r & 7)) is 2-way on the b128 row read; the 32-byte-block one conflicts on it.
+// D = 64 (128-byte rows): dsw = {r1, r2, r1 ^ r3}; D = 128 (256-byte rows): dsw = (r & 3) << 2 | (r >> 2) & 3.
+template <int D> __device__ __forceinline__ int dsw(int r) {
+  if constexpr (D == 64) return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | ((((r >> 1) ^ (r >> 3)) & 1) << 2);
+  else return ((r & 3) << 2) | ((r >> 2) & 3);
+}
+template <int D> __device__ __forceinline__ int dual_off(int r, int col) {   // col: a multiple of 4 for tr reads
+  return r * (D * 2) + (((col >> 3) ^ dsw<D>(r)) << 4) + ((col & 7) << 1);
+}
+// lane-constant byte offsets of the dual-image reads of a 32-row sub-tile at row 0 (rows 32u.. and the second
+// 16-row half add multiples of 16 rows, which leave dsw unchanged): row reads of chunk 2s + h, and the two
+// ds_read_b64_tr_b16 halves (e = 0: rows 4h + q, e = 1: rows 8 + 4h + q) of column block dt
+template <int D> struct DualOffs {
+  int row[D / 16];
+  int tr[D / 32][2];
+  __device__ __forceinline__ void prepare() {
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) row[s] = r * (D * 2) + (((2 * s + h) ^ dsw<D>(r)) << 4);
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) tr[dt][e] = dual_off<D>(4 * h + q + 8 * e, dt * 32 + 16 * (G & 1) + 4 * p);
+  }
+  // row fragment s of the sub-tile whose first row is `row0` (a multiple of 16)
+  __device__ __forceinline__ bf16x8 rowf(const char* img, int row0, int s) const {
+    return *reinterpret_cast<const bf16x8*>(img + row0 * (D * 2) + row[s]);
+  }
+  // tr_frag's operand (rows row0 + 16 s ..) of column block dt
+  __device__ __forceinline__ bf16x8 trf(const char* img, int row0, int s, int dt) const {
+    const char* base = img + (row0 + 16 * s) * (D * 2);
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + tr[dt][0]));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + tr[dt][1]));
+    short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+};
+
 // x ~= t0 + t1 + t2 (bf16 each, round-to-nearest at every stage): returns {t0 | t1 << 16, t2}
 __device__ __forceinline__ uint2 split3_bf16(float x) {
   const bf16_t t0 = f2bf(x);
@@ -208,9 +251,11 @@ __device__ __forceinline__ void stage_loop(int ntiles, F&& step) {
   }
 }
 
-// DMA geometry of one [ROWS x D] bf16 image (row or transposed-read swizzle), split over 4 waves:
-// piece p (1 KiB) = wave + 4 i; lane l writes bytes [16 l, 16 l + 16) of the piece.
-template <int D, int ROWS, bool TR>
+// DMA geometry of one [ROWS x D] bf16 image, split over 4 waves: piece p (1 KiB) = wave + 4 i; lane l writes
+// bytes [16 l, 16 l + 16) of the piece.  MODE: IMG_ROW (chunk ^ (r & 7)), IMG_TR (32-byte block ^ tr_sw), IMG_DUAL
+// (chunk ^ dsw: row and transposed reads of one copy).
+constexpr int IMG_ROW = 0, IMG_TR = 1, IMG_DUAL = 2;
+template <int D, int ROWS, int MODE>
 struct DmaImg {
   static constexpr int RB = D * 2;
   static constexpr int NP = ROWS * RB / 1024;
@@ -223,7 +268,8 @@ struct DmaImg {
       const int byte = (wave + 4 * i) * 1024 + lane * 16;
       const int r = byte / RB, pos = (byte % RB) >> 4;
       row[i] = r;
-      col[i] = TR ? ((((pos >> 1) ^ tr_sw<D>(r)) << 4) + ((pos & 1) << 3)) : ((pos ^ (r & 7)) << 3);
+      col[i] = MODE == IMG_TR ? ((((pos >> 1) ^ tr_sw<D>(r)) << 4) + ((pos & 1) << 3))
+                              : ((pos ^ (MODE == IMG_DUAL ? dsw<D>(r) : (r & 7))) << 3);
     }
   }
   // rows [row0, row0 + ROWS) of a [nrows x ld] operand whose descriptor starts at (batch, head)
@@ -284,8 +330,8 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = KT * D * 2;      // bytes of one [64 x D] image
   constexpr int STG = 2 * TB;         // K row image + V transposed-read image
-  using KImg = DmaImg<D, KT, false>;
-  using VImg = DmaImg<D, KT, true>;
+  using KImg = DmaImg<D, KT, IMG_DUAL>;   // row reads only; the dual swizzle is conflict-free for them
+  using VImg = DmaImg<D, KT, IMG_TR>;
   constexpr int LOADS = KImg::PW + VImg::PW;
   int bx, hh, b;
   block_ids(a, bx, hh, b);
@@ -299,6 +345,8 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
   VImg vi;
   ki.prepare(wave, lane);
   vi.prepare(wave, lane);
+  DualOffs<D> dof;
+  dof.prepare();
   const int ntiles = (a.Nk + KT - 1) / KT;
 
   bf16x8 qf[D / 16];
@@ -336,7 +384,7 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
       if (t * KT + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile (Lk = 77): P = 0
       float16v S = zero16();
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) S = mfma32(lds_row_frag(kimg, D * 2, sub * 32 + r, 2 * s + h), qf[s], S);
+      for (int s = 0; s < D / 16; ++s) S = mfma32(dof.rowf(kimg, sub * 32, s), qf[s], S);
       const int kbase = t * KT + sub * 32;
       if (kbase + 32 > a.Nk) {
 #pragma unroll
@@ -404,7 +452,8 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
   if (q < a.Nq && h == 0 && a.lse) a.lse[((long long)b * a.H + hh) * a.Nq + q] = m + __log2f(l);
 }
 
-// dQ: per wave 32 queries, iterate over key tiles (K row + K transposed + V row images per stage)
+// dQ: per wave 32 queries, iterate over key tiles (a dual-use K image -- row reads for S, transposed reads for
+// dQ -- and a V image per stage)
 // NS = LDS ring depth, KTD = keys per tile.  D = 128 runs 32-key tiles 3 deep (72 KiB): two blocks
 // per CU (the 64-key 3-deep ring, 144 KiB, left one block -- one wave per SIMD).  D = 64 with NS = 2 (48 KiB) lets three blocks share a CU (150 VGPRs fit three
 // waves per SIMD), so the SDXL level-2 grid (8 x 20 heads x 4 = 640 blocks) runs in one round of
@@ -413,10 +462,9 @@ template <int D, int NS, int KTD = KT>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = KTD * D * 2;
-  constexpr int STG = 3 * TB;
-  using RImg = DmaImg<D, KTD, false>;
-  using TImg = DmaImg<D, KTD, true>;
-  constexpr int LOADS = 2 * RImg::PW + TImg::PW;
+  constexpr int STG = 2 * TB;
+  using Img = DmaImg<D, KTD, IMG_DUAL>;
+  constexpr int LOADS = 2 * Img::PW;
   int bx, hh, b;
   block_ids(a, bx, hh, b);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -424,15 +472,14 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   const int q0 = bx * 128 + wave * 32;
   const auto rk = rsrc(a.k + b * a.bsk + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldk + a.Dv) * 2);
   const auto rv = rsrc(a.v + b * a.bsv + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldv + a.Dv) * 2);
-  RImg ri;
-  TImg ti;
-  ri.prepare(wave, lane);
-  ti.prepare(wave, lane);
+  Img im;
+  im.prepare(wave, lane);
+  DualOffs<D> dof;
+  dof.prepare();
   const int ntiles = (a.Nk + KTD - 1) / KTD;
   auto issue = [&](int t, char* st) {
-    ri.issue(rk, st, a.ldk, t * KTD, a.Nk, a.Dv, wave);
-    ti.issue(rk, st + TB, a.ldk, t * KTD, a.Nk, a.Dv, wave);
-    ri.issue(rv, st + 2 * TB, a.ldv, t * KTD, a.Nk, a.Dv, wave);
+    im.issue(rk, st, a.ldk, t * KTD, a.Nk, a.Dv, wave);
+    im.issue(rv, st + TB, a.ldv, t * KTD, a.Nk, a.Dv, wave);
   };
 
   bf16x8 qf[D / 16], gf[D / 16];
@@ -490,9 +537,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
     else wait_vmcnt<0>();
     BARRIER();
     if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
-    const char* krow = smem + SI * STG;
-    const char* ktr = krow + TB;
-    const char* vrow = krow + 2 * TB;
+    const char* kimg = smem + SI * STG;
+    const char* vimg = kimg + TB;
 #pragma unroll
     for (int sub = 0; sub < KTD / 32; ++sub) {
       if (t * KTD + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile: dS = 0
@@ -501,8 +547,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
       float16v S = zero16(), dP = ndl;
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
-        S = mfma32(lds_row_frag(krow, D * 2, sub * 32 + r, 2 * s + h), qf[s], S);
-        dP = mfma32(lds_row_frag(vrow, D * 2, sub * 32 + r, 2 * s + h), gf[s], dP);
+        S = mfma32(dof.rowf(kimg, sub * 32, s), qf[s], S);
+        dP = mfma32(dof.rowf(vimg, sub * 32, s), gf[s], dP);
       }
       const int kbase = t * KTD + sub * 32;
       if (kbase + 32 > a.Nk) {
@@ -516,8 +562,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
       const bf16x8 s0 = pack_acc(S, 0), s1 = pack_acc(S, 1);
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
-        dQ[dt] = mfma32(tr_frag<D>(ktr, sub * 32, 0, dt * 32), s0, dQ[dt]);
-        dQ[dt] = mfma32(tr_frag<D>(ktr, sub * 32, 1, dt * 32), s1, dQ[dt]);
+        dQ[dt] = mfma32(dof.trf(kimg, sub * 32, 0, dt), s0, dQ[dt]);
+        dQ[dt] = mfma32(dof.trf(kimg, sub * 32, 1, dt), s1, dQ[dt]);
       }
     }
   };
@@ -527,29 +573,30 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   for (int dt = 0; dt < D / 32; ++dt) store_tile_bf16(Dp, dt * 32, dQ[dt], a.scale, a.Dv, q < a.Nq);
 }
 
-// dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of 32 in this split's range.
-// Stage: Q row, Q transposed, dO row, dO transposed images + the tile's 32 bias records (written by the dQ
-// kernel: -lse/c and -delta as three bf16 terms each).  The record is one extra MFMA k-step of S and of dP
-// (A = the record of the lane's query, B = ones in the matching three k slots), so the accumulators come out as
-// S - lse/c and dP - delta: no per-score subtraction and no per-register {lse, delta} reads in the softmax.
-// D = 128: the dK/dV accumulators alone take 128 VGPRs and the 3-deep ring (99 KiB) already limits a
-// CU to one block, so the full 512-entry register file is used instead of spilling at 256.
+// dK, dV: per wave 32 keys (block 128 keys), iterate over query tiles of QS (32 or 64) in this split's range.
+// Stage: dual-use Q and dO images (row reads for S / dP, transposed reads for dK / dV: one copy each) + the tile's
+// QS bias records (written by the dQ kernel: -lse/c and -delta as three bf16 terms each).  The record is one extra
+// MFMA k-step of S and of dP (A = the record of the lane's query, B = ones in the matching three k slots), so the
+// accumulators come out as S - lse/c and dP - delta: no per-score subtraction and no per-register {lse, delta}
+// reads in the softmax.  A 64-query stage runs two 32-query sub-tiles per barrier.
+// D = 128: the dK/dV accumulators alone take 128 VGPRs, so the full 512-entry register file is used (one wave
+// per SIMD) instead of spilling at 256.
 // (A software-pipelined D = 128 variant -- S / dP of tile t+1 on the MFMA pipe during tile t's
 // softmax, 4-deep ring -- measured slower: 1487-1510 vs 1349 us for the Flux bwd; not kept.)
 // OCC = waves per SIMD.  D = 64 at OCC = 3 (<= 168 VGPRs: the tile loop not unrolled) fits 768 blocks on
 // the chip, the SDXL level-2 grid (8 key blocks x 20 heads x 4 = 640) in one round instead of 1.25 at OCC 2.
-template <int D> constexpr int dkv_stage() { return 4 * QT * D * 2 + QT * 16; }
-template <int D> constexpr int dkv_lds() { return 3 * dkv_stage<D>(); }   // the kernel's 3-deep ring
+template <int D, int QS> constexpr int dkv_stage() { return 2 * QS * D * 2 + QS * 16; }
+template <int D, int QS> constexpr int dkv_lds() { return 3 * dkv_stage<D, QS>(); }   // the kernel's 3-deep ring
 
-template <int D, int OCC = 1>
+template <int D, int OCC, int QS>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TB = QT * D * 2;                 // one [32 x D] image
-  constexpr int STG = dkv_stage<D>();            // 4 images + 32 16-byte bias records
-  constexpr int NS = 3;                          // 50 KiB (D = 64): 3 blocks per CU
-  using RImg = DmaImg<D, QT, false>;
-  using TImg = DmaImg<D, QT, true>;
-  constexpr int LOADS = 2 * RImg::PW + 2 * TImg::PW + 1;
+  constexpr int TB = QS * D * 2;                 // one [QS x D] image
+  constexpr int STG = dkv_stage<D, QS>();        // Q + dO images + QS 16-byte bias records
+  constexpr int NS = 3;
+  constexpr int RPW = QS / 4;                    // bias records moved per wave
+  using Img = DmaImg<D, QS, IMG_DUAL>;
+  constexpr int LOADS = 2 * Img::PW + 1;
   int bx, hh, bz;
   block_ids(a, bx, hh, bz);
   const int b = bz / a.qsplit, split = bz % a.qsplit;
@@ -560,25 +607,23 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
   const auto rq = rsrc(a.q + b * a.bsq + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldq + a.Dv) * 2);
   const auto rg = rsrc(a.dout + b * a.bsdo + hh * a.Dv, ((long long)(a.Nq - 1) * a.lddo + a.Dv) * 2);
   const auto rp = rsrc(a.delta + 4 * srow, (long long)a.Nq * 16);
-  RImg ri;
-  TImg ti;
-  ri.prepare(wave, lane);
-  ti.prepare(wave, lane);
+  Img im;
+  im.prepare(wave, lane);
+  DualOffs<D> dof;
+  dof.prepare();
 
-  const int per = (((a.Nq + a.qsplit - 1) / a.qsplit) + QT - 1) / QT * QT;
+  const int per = (((a.Nq + a.qsplit - 1) / a.qsplit) + QS - 1) / QS * QS;
   const int qbeg = split * per;
   const int qend = min(a.Nq, qbeg + per);
-  const int ntiles = qend > qbeg ? (qend - qbeg + QT - 1) / QT : 0;
+  const int ntiles = qend > qbeg ? (qend - qbeg + QS - 1) / QS : 0;
   auto issue = [&](int t, char* st) {
-    const int qt0 = qbeg + t * QT;
-    ri.issue(rq, st, a.ldq, qt0, qend, a.Dv, wave);
-    ti.issue(rq, st + TB, a.ldq, qt0, qend, a.Dv, wave);
-    ri.issue(rg, st + 2 * TB, a.lddo, qt0, qend, a.Dv, wave);
-    ti.issue(rg, st + 3 * TB, a.lddo, qt0, qend, a.Dv, wave);
-    if (lane < 8) {   // 32 records of 16 B; wave w moves records 8w .. 8w+7
-      const int qr = qt0 + 8 * wave + lane;
+    const int qt0 = qbeg + t * QS;
+    im.issue(rq, st, a.ldq, qt0, qend, a.Dv, wave);
+    im.issue(rg, st + TB, a.lddo, qt0, qend, a.Dv, wave);
+    if (lane < RPW) {   // QS records of 16 B; wave w moves records RPW w .. RPW w + RPW - 1
+      const int qr = qt0 + RPW * wave + lane;
       const unsigned off = qr < qend ? (unsigned)qr * 16u : OFF_INVALID;
-      dma16(rp, st + 4 * TB + 128 * wave, off);
+      dma16(rp, st + 2 * TB + 16 * RPW * wave, off);
     }
   };
 
@@ -603,20 +648,19 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
     ones_s[j] = (__bf16)((h == 0 && j < 3) ? 1.f : 0.f);
     ones_d[j] = (__bf16)((h == 0 && j >= 3 && j < 6) ? 1.f : 0.f);
   }
-  // S' = Q K^T - lse/c and dP' = dO V^T - delta of one query tile (key on the lane)
-  auto sdp = [&](float16v& S_, float16v& dP_, const char* st) {
-    const bf16x8 rec = *reinterpret_cast<const bf16x8*>(st + 4 * TB + r * 16);   // this lane's query
+  // S' = Q K^T - lse/c and dP' = dO V^T - delta of the 32-query sub-tile at row u0 of the stage (key on the lane)
+  auto sdp = [&](float16v& S_, float16v& dP_, const char* st, int u0) {
+    const bf16x8 rec = *reinterpret_cast<const bf16x8*>(st + 2 * TB + (u0 + r) * 16);   // this lane's query
     S_ = mfma32(rec, ones_s, zero16());
     dP_ = mfma32(rec, ones_d, zero16());
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
-      S_ = mfma32(lds_row_frag(st, D * 2, r, 2 * s + h), kf[s], S_);
-      dP_ = mfma32(lds_row_frag(st + 2 * TB, D * 2, r, 2 * s + h), vf[s], dP_);
+      S_ = mfma32(dof.rowf(st, u0, s), kf[s], S_);
+      dP_ = mfma32(dof.rowf(st + TB, u0, s), vf[s], dP_);
     }
   };
   // P = exp2(S' c), dS = P dP', packed as the dV / dK B operands
-  auto softmax_pack = [&](float16v& S, float16v& dP, const char* st, bf16x8 (&pk)[4]) {
-    (void)st;
+  auto softmax_pack = [&](float16v& S, float16v& dP, bf16x8 (&pk)[4]) {
     if constexpr (D == 64) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -645,18 +689,15 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
     pk[3] = pack_acc(dP, 1);
   };
   // dV^T += dO^T P, dK^T += Q^T dS
-  auto dvdk = [&](const char* st, const bf16x8 (&pk)[4]) {
-    const char* qtr = st + TB;
-    const char* gtr = st + 3 * TB;
+  auto dvdk = [&](const char* st, int u0, const bf16x8 (&pk)[4]) {
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt) {
-      dV[dt] = mfma32(tr_frag<D>(gtr, 0, 0, dt * 32), pk[0], dV[dt]);
-      dV[dt] = mfma32(tr_frag<D>(gtr, 0, 1, dt * 32), pk[1], dV[dt]);
-      dK[dt] = mfma32(tr_frag<D>(qtr, 0, 0, dt * 32), pk[2], dK[dt]);
-      dK[dt] = mfma32(tr_frag<D>(qtr, 0, 1, dt * 32), pk[3], dK[dt]);
+      dV[dt] = mfma32(dof.trf(st + TB, u0, 0, dt), pk[0], dV[dt]);
+      dV[dt] = mfma32(dof.trf(st + TB, u0, 1, dt), pk[1], dV[dt]);
+      dK[dt] = mfma32(dof.trf(st, u0, 0, dt), pk[2], dK[dt]);
+      dK[dt] = mfma32(dof.trf(st, u0, 1, dt), pk[3], dK[dt]);
     }
   };
-
 
   auto step = [&](int t, auto si_tag) {
     const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
@@ -665,11 +706,15 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
     BARRIER();
     if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
     const char* st = smem + SI * STG;
-    float16v S, dP;
-    bf16x8 pk[4];
-    sdp(S, dP, st);
-    softmax_pack(S, dP, st, pk);
-    dvdk(st, pk);
+#pragma unroll 1
+    for (int u = 0; u < QS / 32; ++u) {
+      if (u > 0 && qbeg + t * QS + 32 * u >= qend) break;   // a wholly padded sub-tile of the last stage
+      float16v S, dP;
+      bf16x8 pk[4];
+      sdp(S, dP, st, 32 * u);
+      softmax_pack(S, dP, pk);
+      dvdk(st, 32 * u, pk);
+    }
   };
   stage_loop<NS, (D <= 64 && OCC < 3)>(ntiles, step);
   const int key = k0 + r;
@@ -705,10 +750,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
 // pass instead of the dQ + dK/dV pair (which recompute S and dP, stream Q / dO twice and need a query split for
 // dK/dV parallelism over one key block).  Workgroup = (query chunk, head, batch), 4 waves; wave w owns keys
 // 32w .. 32w+31: their K / V row fragments stay in registers and their dK^T / dV^T accumulators sum over the
-// chunk's queries.  The chunk is walked in rounds of 64 queries, staged by LDS-DMA (Q and dO row + transposed-read
-// images, the O row image).  A round:
+// chunk's queries.  The chunk is walked in rounds of 64 queries, staged by LDS-DMA (dual-use Q and dO images, the O
+// row image).  A round:
 //   delta = rowsum(dO o O) of its 64 queries from the O / dO images (4 lanes per query) -> {lse, delta} table;
-//   S = Q K^T, dP = dO V^T with the key on the lane; P = exp2(S c - lse), dS = P (dP - delta) feed
+//   S = Q K^T, dP = dO V^T with the key on the lane (row reads of the dual-use Q / dO images); P = exp2(S c - lse),
+//   dS = P (dP - delta) feed
 //   dV^T += dO^T P and dK^T += Q^T dS as MFMA B operands; dS^T (bf16) -> an LDS [key][query] image;
 //   dQ^T = K^T dS^T: one (32 d x 32 q) tile per wave over the active keys (stored at the next round's start).
 // 5 MFMA products per (query, key) tile instead of 7.  dK / dV: bf16 directly with one chunk, else fp32 per-chunk
@@ -716,11 +762,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
 constexpr int XQR = 64;   // queries per round
 constexpr int XIMG = XQR * 64 * 2;                      // one [64 x 64] bf16 image
 constexpr int X_KTR = 0;                                // K transposed-read image, 128 keys (16 KiB)
-constexpr int X_QROW = 16384, X_QTR = X_QROW + XIMG, X_GROW = X_QTR + XIMG, X_GTR = X_GROW + XIMG,
-              X_OROW = X_GTR + XIMG;
+constexpr int X_QIMG = 16384, X_GIMG = X_QIMG + XIMG;  // dual-use Q / dO images (row AND transposed reads)
+constexpr int X_OROW = X_GIMG + XIMG;                   // O row image (delta)
 constexpr int X_DST = X_OROW + XIMG;                    // dS^T image [128 keys][64 queries] (16 KiB)
 constexpr int X_PAIRS = X_DST + 16384;                  // 64 {lse, delta}
-constexpr int X_LDS = X_PAIRS + XQR * 8;                // 72.5 KiB: two workgroups per CU
+constexpr int X_LDS = X_PAIRS + XQR * 8;                // 56.5 KiB: two workgroups per CU (189 VGPRs)
 
 __device__ __forceinline__ int cross_per(const AttnArgs& a) {
   return ((a.Nq + a.qsplit - 1) / a.qsplit + XQR - 1) / XQR * XQR;
@@ -729,9 +775,9 @@ __device__ __forceinline__ int cross_per(const AttnArgs& a) {
 __global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int D = 64;
-  using RImg = DmaImg<D, XQR, false>;
-  using TImg = DmaImg<D, XQR, true>;
-  using KImg = DmaImg<D, 128, true>;
+  using QImg = DmaImg<D, XQR, IMG_DUAL>;
+  using RImg = DmaImg<D, XQR, IMG_ROW>;
+  using KImg = DmaImg<D, 128, IMG_TR>;
   int chunk, hh, b;
   block_ids(a, chunk, hh, b);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -745,17 +791,17 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
   const auto rg = rsrc(a.dout + b * a.bsdo + hh * a.Dv, ((long long)(a.Nq - 1) * a.lddo + a.Dv) * 2);
   const auto ro = rsrc(a.o + b * a.bso + hh * a.Dv, ((long long)(a.Nq - 1) * a.ldo + a.Dv) * 2);
   const auto rk = rsrc(a.k + b * a.bsk + hh * a.Dv, ((long long)(a.Nk - 1) * a.ldk + a.Dv) * 2);
+  QImg qi;
   RImg ri;
-  TImg ti;
   KImg kti;
+  qi.prepare(wave, lane);
   ri.prepare(wave, lane);
-  ti.prepare(wave, lane);
   kti.prepare(wave, lane);
+  DualOffs<D> dof;
+  dof.prepare();
   auto issue = [&](int q0) {   // rows >= qend (the next chunk's, or past Nq) are zero-filled
-    ri.issue(rq, smem + X_QROW, a.ldq, q0, qend, a.Dv, wave);
-    ti.issue(rq, smem + X_QTR, a.ldq, q0, qend, a.Dv, wave);
-    ri.issue(rg, smem + X_GROW, a.lddo, q0, qend, a.Dv, wave);
-    ti.issue(rg, smem + X_GTR, a.lddo, q0, qend, a.Dv, wave);
+    qi.issue(rq, smem + X_QIMG, a.ldq, q0, qend, a.Dv, wave);
+    qi.issue(rg, smem + X_GIMG, a.lddo, q0, qend, a.Dv, wave);
     ri.issue(ro, smem + X_OROW, a.ldo, q0, qend, a.Dv, wave);
   };
   const int key0 = wave * 32;
@@ -794,7 +840,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
       for (int c2 = 0; c2 < 2; ++c2) {
         const int ch = 2 * dpart + c2;
         const bf8 ov = *reinterpret_cast<const bf8*>(smem + X_OROW + dqi * 128 + ((ch ^ (dqi & 7)) << 4));
-        const bf8 gv = *reinterpret_cast<const bf8*>(smem + X_GROW + dqi * 128 + ((ch ^ (dqi & 7)) << 4));
+        const bf8 gv = *reinterpret_cast<const bf8*>(smem + X_GIMG + dqi * 128 + ((ch ^ dsw<D>(dqi)) << 4));
         float of[8], gf[8];
         unpack8(ov, of);
         unpack8(gv, gf);
@@ -812,8 +858,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
         float16v S = zero16(), dP = zero16();
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          S = mfma32(lds_row_frag(smem + X_QROW, D * 2, qt * 32 + r, 2 * s + h), kf[s], S);
-          dP = mfma32(lds_row_frag(smem + X_GROW, D * 2, qt * 32 + r, 2 * s + h), vf[s], dP);
+          S = mfma32(dof.rowf(smem + X_QIMG, qt * 32, s), kf[s], S);
+          dP = mfma32(dof.rowf(smem + X_GIMG, qt * 32, s), vf[s], dP);
         }
         const float4* pv = reinterpret_cast<const float4*>(smem + X_PAIRS) + qt * 16;   // pairs 2j, 2j+1
 #pragma unroll
@@ -836,10 +882,10 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
         const bf16x8 p0 = pack_acc(S, 0), p1 = pack_acc(S, 1), d0 = pack_acc(dP, 0), d1 = pack_acc(dP, 1);
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt) {
-          dV[dt] = mfma32(tr_frag<D>(smem + X_GTR, qt * 32, 0, dt * 32), p0, dV[dt]);
-          dV[dt] = mfma32(tr_frag<D>(smem + X_GTR, qt * 32, 1, dt * 32), p1, dV[dt]);
-          dK[dt] = mfma32(tr_frag<D>(smem + X_QTR, qt * 32, 0, dt * 32), d0, dK[dt]);
-          dK[dt] = mfma32(tr_frag<D>(smem + X_QTR, qt * 32, 1, dt * 32), d1, dK[dt]);
+          dV[dt] = mfma32(dof.trf(smem + X_GIMG, qt * 32, 0, dt), p0, dV[dt]);
+          dV[dt] = mfma32(dof.trf(smem + X_GIMG, qt * 32, 1, dt), p1, dV[dt]);
+          dK[dt] = mfma32(dof.trf(smem + X_QIMG, qt * 32, 0, dt), d0, dK[dt]);
+          dK[dt] = mfma32(dof.trf(smem + X_QIMG, qt * 32, 1, dt), d1, dK[dt]);
         }
         // dS^T -> the [key][query] transposed-read image: registers 4g..4g+3 are 4 consecutive queries
         const uint4 w0 = __builtin_bit_cast(uint4, d0), w1 = __builtin_bit_cast(uint4, d1);
@@ -1050,11 +1096,11 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   if (cross) {
     launch(attn_bwd_cross_kernel, dim3(qsplit, a.H, a.B), X_LDS, stream, a);
   } else if (a.Dv <= 64) {
-    launch(attn_bwd_dq_kernel<64, 2>, gq, 2 * 3 * KT * 64 * 2, stream, a);
-    launch(attn_bwd_dkv_kernel<64, 3>, gk, dkv_lds<64>(), stream, a);   // SDXL bwd 17.18 -> 16.71 ms/step
+    launch(attn_bwd_dq_kernel<64, 3>, gq, 3 * 2 * KT * 64 * 2, stream, a);
+    launch(attn_bwd_dkv_kernel<64, 3, 64>, gk, dkv_lds<64, 64>(), stream, a);
   } else {
-    launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 3 * 32 * 128 * 2, stream, a);   // 1349 vs 1467 us (64-key tiles)
-    launch(attn_bwd_dkv_kernel<128>, gk, dkv_lds<128>(), stream, a);
+    launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 2 * 32 * 128 * 2, stream, a);   // 1349 vs 1467 us (64-key tiles)
+    launch(attn_bwd_dkv_kernel<128, 1, 64>, gk, dkv_lds<128, 64>(), stream, a);
   }
   OTAMD_CHECK_LAUNCH();
   if (qsplit > 1) {
