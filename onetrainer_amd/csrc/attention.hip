@@ -250,6 +250,31 @@ __device__ __forceinline__ void stage_loop(int ntiles, F&& step) {
     for (int t = 0; t < ntiles; ++t) step(t, t % NS);
   }
 }
+// The same with the last tile apart: step(t, slot, std::bool_constant<last>).  Only the last key tile can hold keys
+// past Nk, so the per-score tail mask is compiled into that copy alone (in a shared body the compiler if-converts
+// the uniform `tile is partial` branch into 32 compares / selects on every tile).
+template <typename F, int... I>
+__device__ __forceinline__ void stage_steps_nl(int t, F& step, std::integer_sequence<int, I...>) {
+  (step(t + I, std::integral_constant<int, I>{}, std::false_type{}), ...);
+}
+template <typename F, int... I>
+__device__ __forceinline__ void stage_tail_nl(int t, int n, F& step, std::integer_sequence<int, I...>) {
+  ((t + I < n ? step(t + I, std::integral_constant<int, I>{}, std::false_type{}) : void()), ...);
+}
+template <int NS, bool UNROLL = true, typename F>
+__device__ __forceinline__ void stage_loop_last(int ntiles, F&& step) {
+  if (ntiles <= 0) return;
+  const int nmain = ntiles - 1;
+  if constexpr (UNROLL) {
+    int t = 0;
+    for (; t + NS <= nmain; t += NS) stage_steps_nl(t, step, std::make_integer_sequence<int, NS>{});
+    stage_tail_nl(t, nmain, step, std::make_integer_sequence<int, NS - 1>{});
+    step(nmain, nmain % NS, std::true_type{});   // one copy with a run-time ring slot
+  } else {
+    for (int t = 0; t < nmain; ++t) step(t, t % NS, std::false_type{});
+    step(nmain, nmain % NS, std::true_type{});
+  }
+}
 
 // DMA geometry of one [ROWS x D] bf16 image, split over 4 waves: piece p (1 KiB) = wave + 4 i; lane l writes
 // bytes [16 l, 16 l + 16) of the piece.  MODE: IMG_ROW (chunk ^ (r & 7)), IMG_TR (32-byte block ^ tr_sw), IMG_DUAL
@@ -366,8 +391,9 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
   for (int t = 0; t < D / 32; ++t) O[t] = zero16();
   float m = -INFINITY, l = 0.f;
 
-  auto step = [&](int t, auto si_tag) {
+  auto step = [&](int t, auto si_tag, auto last_tag) {
     const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
+    constexpr bool LAST = decltype(last_tag)::value;
 
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
@@ -381,12 +407,12 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
     const char* vimg = kimg + TB;
 #pragma unroll
     for (int sub = 0; sub < KT / 32; ++sub) {
-      if (t * KT + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile (Lk = 77): P = 0
+      if (LAST && t * KT + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile (Lk = 77): P = 0
       float16v S = zero16();
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) S = mfma32(dof.rowf(kimg, sub * 32, s), qf[s], S);
       const int kbase = t * KT + sub * 32;
-      if (kbase + 32 > a.Nk) {
+      if (LAST && kbase + 32 > a.Nk) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           if (kbase + acc_row(i, h) >= a.Nk) S[i] = -INFINITY;
@@ -443,7 +469,7 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
       }
     }
   };
-  stage_loop<NS, (D <= 64)>(ntiles, step);
+  stage_loop_last<NS, (D <= 64)>(ntiles, step);
   const int q = q0 + r;
   const float inv = 1.f / l;
   bf16_t* Op = a.o + b * a.bso + (long long)min(q, a.Nq - 1) * a.ldo + hh * a.Dv;
@@ -459,7 +485,7 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
 // waves per SIMD), so the SDXL level-2 grid (8 x 20 heads x 4 = 640 blocks) runs in one round of
 // 768 slots instead of 1.25 rounds of 512 with NS = 3 (72 KiB).
 template <int D, int NS, int KTD = KT>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, D == 64 ? 3 : 2) attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TB = KTD * D * 2;
   constexpr int STG = 2 * TB;
@@ -530,8 +556,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dQ[t] = zero16();
 
-  auto step = [&](int t, auto si_tag) {
+  auto step = [&](int t, auto si_tag, auto last_tag) {
     const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
+    constexpr bool LAST = decltype(last_tag)::value;
 
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
@@ -541,7 +568,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
     const char* vimg = kimg + TB;
 #pragma unroll
     for (int sub = 0; sub < KTD / 32; ++sub) {
-      if (t * KTD + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile: dS = 0
+      if (LAST && t * KTD + sub * 32 >= a.Nk) break;   // a wholly masked 32-key half of the last tile: dS = 0
       // dP^T starts from -delta (this lane's query: a per-lane constant vector built once), so
       // dS^T = P^T dP'^T needs no subtraction per score
       float16v S = zero16(), dP = ndl;
@@ -551,7 +578,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
         dP = mfma32(dof.rowf(vimg, sub * 32, s), gf[s], dP);
       }
       const int kbase = t * KTD + sub * 32;
-      if (kbase + 32 > a.Nk) {
+      if (LAST && kbase + 32 > a.Nk) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           if (kbase + acc_row(i, h) >= a.Nk) S[i] = -INFINITY;
@@ -567,7 +594,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
       }
     }
   };
-  stage_loop<NS, (D <= 64)>(ntiles, step);
+  stage_loop_last<NS, (D <= 64)>(ntiles, step);
   bf16_t* Dp = a.dq + b * a.bsdq + (long long)min(q, a.Nq - 1) * a.lddq + hh * a.Dv;
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) store_tile_bf16(Dp, dt * 32, dQ[dt], a.scale, a.Dv, q < a.Nq);
