@@ -129,6 +129,15 @@ int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_
    per-chunk dK/dV partials) */
 long long otamd_attn_bwd_ws_bytes(const AttnArgs* in);
 
+/* bytes of the fp32 dK / dV partial slabs alone (0: none needed), the caller-owned buffer of otamd_attn_bwd_ex */
+long long otamd_attn_bwd_slab_bytes(const AttnArgs* in);
+
+/* replaces: as otamd_attn_bwd (autograd of scaled_dot_product_attention, GenericTrainer.py:693-696), with the dK / dV
+   partial slabs in a caller-owned buffer and their chunk-order sum on cast_stream (ordered after `stream` by an
+   event): the one-pass cross-attention backward's dK / dV feed only the K / V projections' weight gradients */
+int otamd_attn_bwd_ex(const AttnArgs* in, float* ws, long long ws_bytes, float* slabs, long long slab_bytes,
+                      hipStream_t stream, hipStream_t cast_stream);
+
 /* replaces: ABI check */
 int otamd_attn_args_size(void);
 

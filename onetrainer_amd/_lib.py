@@ -107,6 +107,8 @@ SIGNATURES: dict[str, list] = {
     "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],
     "otamd_attn_bwd": [C.POINTER(AttnArgs), VP, LL, VP],
     "otamd_attn_bwd_ws_bytes": [C.POINTER(AttnArgs)],
+    "otamd_attn_bwd_slab_bytes": [C.POINTER(AttnArgs)],
+    "otamd_attn_bwd_ex": [C.POINTER(AttnArgs), VP, LL, VP, LL, VP, VP],
     # softmax.hip (materialized attention for heads > 128)
     "otamd_softmax_rows_fwd": [VP, LL, VP, LL, VP, LL, I, I, F, VP],
     "otamd_softmax_rows_bwd": [VP, LL, VP, LL, VP, LL, LL, I, I, F, VP],
@@ -174,7 +176,7 @@ def lib():
                 continue
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_plan", "_part_floats")) else C.c_int
+            fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_slab_bytes", "_plan", "_part_floats")) else C.c_int
         _lib = L
     return _lib
 

@@ -844,7 +844,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
   for (int s = 0; s < D / 16; ++s) { consume(kf[s]); consume(vf[s]); }
   consume(lse_n);
   const float c = a.scale * LOG2E;
-  const bool kvalid = key0 + r < a.Nk;
 
   float16v dK[D / 32], dV[D / 32], dQ = zero16();
 #pragma unroll
@@ -897,9 +896,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_cross_kernel(AttnArgs a) {
           for (int e = 0; e < 2; ++e) {
             const float4 pp = e ? p23 : p01;
             const int i0 = 4 * g + 2 * e;
-            float p0 = __builtin_amdgcn_exp2f(fmaf(S[i0], c, -pp.x));
-            float p1 = __builtin_amdgcn_exp2f(fmaf(S[i0 + 1], c, -pp.z));
-            if (!kvalid) p0 = p1 = 0.f;    // the key is the lane: padded keys contribute nothing
+            // padded keys (the lane past Nk: zero K / V fragments) get a finite P <= 1 (the clamp, folded into
+            // v_exp_f32's output modifier) and their dS^T meets zero K rows in dQ = K^T dS^T; their dK / dV are
+            // never stored -- no per-lane select
+            const float p0 = __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(fmaf(S[i0], c, -pp.x)), 0.f, 1.f);
+            const float p1 = __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(fmaf(S[i0 + 1], c, -pp.z)), 0.f, 1.f);
             dP[i0] = p0 * (dP[i0] - pp.y);
             dP[i0 + 1] = p1 * (dP[i0 + 1] - pp.w);
             S[i0] = p0;
@@ -1098,8 +1099,35 @@ static long long attn_ws_bytes(const AttnArgs* in, bool cross) {
 // workspace bytes otamd_attn_bwd needs: 16-byte bias records per query + (split queries) fp32 dK/dV partials
 OTAMD_API long long otamd_attn_bwd_ws_bytes(const AttnArgs* in) { return in ? attn_ws_bytes(in, attn_cross_path(*in)) : -1; }
 
+// bytes of the fp32 dK / dV partial slabs alone (0: these arguments need none) -- the caller-owned `slabs` buffer of
+// otamd_attn_bwd_ex
+OTAMD_API long long otamd_attn_bwd_slab_bytes(const AttnArgs* in) {
+  if (!in || in->B <= 0 || in->H <= 0 || in->Nq <= 0 || in->Nk <= 0 || in->Dv <= 0) return -1;
+  const int qs = attn_qsplit(*in, attn_cross_path(*in));
+  return qs > 1 ? 2LL * qs * ((long long)in->B * in->Nk * in->H * in->Dv) * 4 : 0;
+}
+
+static int attn_bwd_impl(const AttnArgs* in, float* ws, long long ws_bytes, float* slabs, long long slab_bytes,
+                         hipStream_t stream, hipStream_t cast_stream);
+
 // ws: otamd_attn_bwd_ws_bytes(args) bytes, 16-byte aligned; lse from the forward
 OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, hipStream_t stream) {
+  return attn_bwd_impl(in, ws, ws_bytes, nullptr, 0, stream, stream);
+}
+
+// As otamd_attn_bwd, with the dK / dV partial slabs in the caller's buffer (otamd_attn_bwd_slab_bytes; ws then needs
+// only the bias records: otamd_attn_bwd_ws_bytes minus the slab bytes) and their chunk-order sum (the cast kernel)
+// on cast_stream, ordered after the main kernels by an event.  For the one-pass cross-attention backward whose dK /
+// dV feed only the K / V projections' weight gradients (module/functional.py CrossAttnFn): the cast leaves the
+// critical stream.  The caller keeps slabs, dk and dv alive until cast_stream has consumed them.
+OTAMD_API int otamd_attn_bwd_ex(const AttnArgs* in, float* ws, long long ws_bytes, float* slabs, long long slab_bytes,
+                                hipStream_t stream, hipStream_t cast_stream) {
+  if (!slabs || ((uintptr_t)slabs & 15)) return OTAMD_EINVAL;
+  return attn_bwd_impl(in, ws, ws_bytes, slabs, slab_bytes, stream, cast_stream);
+}
+
+static int attn_bwd_impl(const AttnArgs* in, float* ws, long long ws_bytes, float* slabs, long long slab_bytes,
+                         hipStream_t stream, hipStream_t cast_stream) {
   if (!in || !attn_ok(*in) || !in->o || !in->lse || !in->dout || !in->dq || !in->dk || !in->dv || !ws) return OTAMD_EINVAL;
   AttnArgs a = *in;
   if (a.lddo % 8 || a.bsdo % 8 || a.lddq % 8 || a.lddk % 8 || a.lddv % 8 || a.bsdq % 8 || a.bsdk % 8 || a.bsdv % 8 ||
@@ -1111,10 +1139,15 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   const long long nkv = (long long)a.B * a.Nk * a.H * a.Dv;
   const int qsplit = attn_qsplit(a, cross);
   a.qsplit = qsplit;
-  if (ws_bytes < attn_ws_bytes(in, cross)) return OTAMD_EINVAL;
+  const long long slab_need = qsplit > 1 ? 2LL * qsplit * nkv * 4 : 0;
+  if (slabs) {
+    if (ws_bytes < attn_ws_bytes(in, cross) - slab_need || slab_bytes < slab_need) return OTAMD_EINVAL;
+  } else if (ws_bytes < attn_ws_bytes(in, cross)) {
+    return OTAMD_EINVAL;
+  }
   a.delta = ws;   // bias records: written by the dQ kernel, read by dK/dV
   if (qsplit > 1) {   // every slab element is written by exactly one block: no memset
-    a.dk32 = ws + ((nrow * 4 + 64) / 64) * 64;
+    a.dk32 = slabs ? slabs : ws + ((nrow * 4 + 64) / 64) * 64;
     a.dv32 = a.dk32 + (long long)qsplit * nkv;
   }
   const int kblocks = (a.Nk + 127) / 128;
@@ -1131,8 +1164,16 @@ OTAMD_API int otamd_attn_bwd(const AttnArgs* in, float* ws, long long ws_bytes, 
   }
   OTAMD_CHECK_LAUNCH();
   if (qsplit > 1) {
+    hipStream_t cs = stream;
+    if (slabs && cast_stream != stream) {   // the sum after the slabs' producer, on the other stream
+      thread_local hipEvent_t ev = nullptr;
+      if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return OTAMD_ELAUNCH;
+      if (hipEventRecord(ev, stream) != hipSuccess || hipStreamWaitEvent(cast_stream, ev, 0) != hipSuccess)
+        return OTAMD_ELAUNCH;
+      cs = cast_stream;
+    }
     int blocks = (int)std::min<long long>((nkv / 4 + 255) / 256, 8192);
-    attn_dkv_cast_kernel<<<blocks, 256, 0, stream>>>(a);
+    attn_dkv_cast_kernel<<<blocks, 256, 0, cs>>>(a);
     OTAMD_CHECK_LAUNCH();
   }
   return OTAMD_OK;

@@ -911,11 +911,15 @@ def attn_fwd(q, k, v, heads, scale=None, out=None):
     return out, lse
 
 
-def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None):
+def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None, cast_stream=None):
+    """cast_stream (a torch stream): where the one-pass cross-attention backward's dK / dV partial slabs are summed
+    (otamd_attn_bwd_ex); dk / dv are then written on that stream, after an event on the current one -- for callers
+    whose dK / dV feed only work queued on cast_stream.  The slabs come from the caching allocator and are
+    record_stream()ed, as are dk / dv."""
     if q.shape[-1] // heads > FLASH_MAX_D:
         return attn_mat_bwd(q, k, v, lse, dout, heads, scale, dq, dk, dv)
     h = _host()
-    if h is not None:
+    if h is not None and cast_stream is None:
         return h.attn_bwd(q, k, v, o, lse, dout, heads, -1.0 if scale is None else scale, dq, dk, dv, stream_handle())
     a = _attn_args(q, k, v, heads, scale)
     dq = torch.empty(q.shape, dtype=BF16, device=q.device) if dq is None else dq
@@ -930,6 +934,16 @@ def attn_bwd(q, k, v, o, lse, dout, heads, scale=None, dq=None, dk=None, dv=None
     a.lddv, a.bsdv = _attn_view(dv, heads)
     nbytes = lib().otamd_attn_bwd_ws_bytes(C.byref(a))
     _req(nbytes > 0, "attention workspace query")
+    sbytes = lib().otamd_attn_bwd_slab_bytes(C.byref(a)) if cast_stream is not None else 0
+    _req(sbytes >= 0, "attention slab query")
+    if sbytes > 0:
+        slabs = torch.empty(sbytes, dtype=torch.uint8, device=q.device)
+        ws = workspace(nbytes - sbytes, q.device)
+        check(lib().otamd_attn_bwd_ex(C.byref(a), _p(ws), nbytes - sbytes, _p(slabs), sbytes, stream_handle(),
+                                      C.c_void_p(cast_stream.cuda_stream)), "otamd_attn_bwd_ex")
+        for t in (slabs, dk, dv):
+            t.record_stream(cast_stream)
+        return dq, dk, dv
     ws = workspace(nbytes, q.device)
     check(lib().otamd_attn_bwd(C.byref(a), _p(ws), nbytes, stream_handle()), "otamd_attn_bwd")
     return dq, dk, dv

@@ -10,6 +10,8 @@ returned gradient is None.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import kernels as K
@@ -465,15 +467,23 @@ class SelfAttnFn(torch.autograd.Function):
         return dqkv, None
 
 
+# the cross-attention dK / dV chunk sum on the weight-gradient stream when only weight gradients consume dkv
+# (OTAMD_CROSS_CAST_SIDE=0: on the current stream, the A/B reference)
+_CROSS_CAST_SIDE = os.environ.get("OTAMD_CROSS_CAST_SIDE", "1") != "0"
+
+
 class CrossAttnFn(torch.autograd.Function):
-    """q [B, N, C], kv [B, L, 2C] -> o [B, N, C]."""
+    """q [B, N, C], kv [B, L, 2C] -> o [B, N, C].  kv_wgrad_only: every consumer of dkv runs on the weight-gradient
+    stream (kv from PrecomputedLinearFn over text states that need no gradient), so the one-pass backward's dK / dV
+    chunk sum (attn_dkv_cast) is queued there too, off the critical stream."""
 
     @staticmethod
-    def forward(ctx, q, kv, heads):
+    def forward(ctx, q, kv, heads, kv_wgrad_only=False):
         C = q.shape[-1]
         o, lse = K.attn_fwd(q, kv[..., :C], kv[..., C:], heads)
         ctx.save_for_backward(q, kv, o, lse)
         ctx.heads = heads
+        ctx.kv_wgrad_only = kv_wgrad_only
         return o
 
     @staticmethod
@@ -483,8 +493,12 @@ class CrossAttnFn(torch.autograd.Function):
         C = q.shape[-1]
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
-        K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:])
-        return dq, (dkv if ctx.needs_input_grad[1] else None), None
+        side = S.side_stream() if (ctx.kv_wgrad_only and _CROSS_CAST_SIDE and ctx.needs_input_grad[1]) else None
+        K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:],
+                   cast_stream=side)
+        if side is not None:
+            dkv.record_stream(side)
+        return dq, (dkv if ctx.needs_input_grad[1] else None), None, None
 
 
 class GEGLUFn(torch.autograd.Function):

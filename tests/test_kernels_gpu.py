@@ -113,6 +113,24 @@ def test_attention(dev, B, Nq, Nk, H, D):
         assert rel_err(got, want.transpose(1, 2).reshape(got.shape)) < 3e-2
 
 
+@pytest.mark.parametrize("B,Nq,Nk,H,D", [(4, 4096, 77, 10, 64), (4, 1024, 77, 20, 64), (2, 300, 77, 4, 40)])
+def test_attention_cross_cast_stream(dev, B, Nq, Nk, H, D):
+    """otamd_attn_bwd_ex: the cross-attention dK / dV chunk sum on another stream (after an event) gives the same
+    bits as the one-stream call; dq is untouched by the move."""
+    torch.manual_seed(6)
+    q, kv = rnd(B, Nq, H * D, dev=dev), rnd(B, Nk, 2 * H * D, dev=dev)
+    k, v = kv[..., :H * D], kv[..., H * D:]
+    o, lse = K.attn_fwd(q, k, v, H)
+    do = rnd(B, Nq, H * D, dev=dev)
+    dq0, dk0, dv0 = K.attn_bwd(q, k, v, o, lse, do, H)
+    side = torch.cuda.Stream(device=dev)
+    for _ in range(3):
+        dkv = torch.full_like(kv, float("nan"))
+        dq, dk, dv = K.attn_bwd(q, k, v, o, lse, do, H, dk=dkv[..., :H * D], dv=dkv[..., H * D:], cast_stream=side)
+        torch.cuda.current_stream().wait_stream(side)
+        assert torch.equal(dq, dq0) and torch.equal(dk, dk0) and torch.equal(dv, dv0)
+
+
 @pytest.mark.parametrize("B,Nq,Nk,H,D,fused", [(2, 256, 256, 8, 160, True), (2, 256, 77, 8, 160, False),
                                                (1, 1024, 1024, 1, 512, False), (3, 64, 64, 2, 160, True),
                                                (2, 300, 77, 8, 80, False)])
