@@ -107,8 +107,30 @@ struct Stage {
     if constexpr (KM) t0 = (lane & 7) ^ ((lane >> 3) & 7);
   }
 
+  // source byte offset of this wave's piece i of the K tile at k0, plain K / MN modes (no conv gather)
+  __device__ __forceinline__ unsigned offset(long long ld, int k0, int Kend, int i) const {
+    static_assert(MODE == OPM_K || MODE == OPM_MN, "plain operand modes");
+    if constexpr (MODE == OPM_K) {
+      const int k = k0 + 8 * t0;
+      return (k < Kend && ok[i]) ? (unsigned)(a[i] + k) * 2u : OFF_INVALID;
+    } else {
+      const int k = k0 + a[i];
+      return (ok[i] && k < Kend) ? (unsigned)(k * (int)ld + b[i]) * 2u : OFF_INVALID;
+    }
+  }
+  // this wave's piece i of the image at img (piece j = wave + NW i); absent pieces of an uneven image are skipped
+  __device__ __forceinline__ void put(__amdgpu_buffer_rsrc_t rs, char* img, int wave, int i, unsigned off) const {
+    if (EVEN || wave + NW * i < NP) dma16(rs, img + (wave + NW * i) * 1024, off);
+  }
   __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* img, const ConvGeom& g, long long ld, int k0,
                                         int Kend, int wave) {
+    unsigned off[NI];
+    offsets(g, ld, k0, Kend, off);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) put(rs, img, wave, i, off[i]);
+  }
+  // source byte offsets of this wave's pieces of the K tile at k0 (OFF_INVALID: zero-fill)
+  __device__ __forceinline__ void offsets(const ConvGeom& g, long long ld, int k0, int Kend, unsigned (&out)[NI]) const {
     if constexpr (KM) {
       const int k = k0 + 8 * t0;
       const bool kok = k < Kend;
@@ -142,7 +164,7 @@ struct Stage {
           }
           if (v) off = (unsigned)(((a[i] * g.SH + sy) * g.SW + sx) * (int)g.ld + ch) * 2u;
         }
-        if (EVEN || wave + NW * i < NP) dma16(rs, img + (wave + NW * i) * 1024, off);
+        out[i] = off;
       }
     } else {
 #pragma unroll
@@ -169,7 +191,7 @@ struct Stage {
           else { v = v && y >= 0 && y < g.SH && x >= 0 && x < g.SW; sy = y; sx = x; }
           if (v) off = (unsigned)(((n * g.SH + sy) * g.SW + sx) * (int)g.ld + c[i]) * 2u;
         }
-        if (EVEN || wave + NW * i < NP) dma16(rs, img + (wave + NW * i) * 1024, off);
+        out[i] = off;
       }
     }
   }
@@ -303,6 +325,32 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
   };
+  // the next half's fragment reads (h = 0, load_b then load_a order) with this wave's refill DMA pieces of the slot
+  // at dst placed one after each read: the inline-asm DMA keeps its place among the DS reads (both touch memory)
+  // while interleave()'s groups put the MFMAs between the reads
+  constexpr int NIA = Stage<AM, BM, NW>::NI, NIB = Stage<BMODE, BN, NW>::NI;
+  constexpr bool SPREAD = !SEG2 && NW == 8 && (AM == OPM_K || AM == OPM_MN) && (BMODE == OPM_K || BMODE == OPM_MN);
+  auto load_ab_refill = [&](bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ], const char* ia, const char* ib, char* dst, int k0) {
+    if constexpr (SPREAD) {
+      auto piece = [&](int t) {   // offsets computed at the piece (no per-step offset arrays: the 256-wide tiles sit
+                                  // at the 256-VGPR cap)
+        if (t < NIA) sa.put(ra, dst, wave, t, sa.offset(args.lda, k0, kend, t));
+        else if (t < NIA + NIB) sb.put(rb, dst + ABYTES, wave, t - NIA, sb.offset(args.ldb, k0, kend, t - NIA));
+      };
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        fb[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 0) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 0);
+        piece(j);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        fa[i] = AK ? frag_k2(ia, wm * TM + i * 16, 0) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 0);
+        piece(NJ + i);
+      }
+#pragma unroll
+      for (int t = MI + NJ; t < NIA + NIB; ++t) piece(t);
+    }
+  };
   // interleave the next fragment reads into the current MFMA block: {2 MFMA, reads of 1 fragment} x (MI+NJ)
   // (128x128: 8 MFMAs per half for 6 fragment reads -> {1 MFMA, reads} x 6, then the rest)
   constexpr int NR = MI + NJ;
@@ -419,7 +467,13 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
   }
 
   int stg = 0;   // ring slot of tile kt (kt % NS)
-  for (int kt = 0; kt < nk; ++kt) {
+  // One K-step.  REFILL: tile kt + NS exists and goes into tile kt's slot.  The plain single-segment K / MN-mode
+  // kernels (SPREAD) place that refill's DMA pieces one after each of phase B's fragment reads: issued as one burst
+  // after the barrier they held the issuing wave for the whole burst (~60-185 cycles per 1-KiB piece,
+  // MI355X_MICROARCH.md) with its MFMAs waiting behind it.  The K steps without a refill (the last NS) run a copy
+  // of the body with no DMA at all, so no branch splits phase B's scheduling region.
+  auto kstep = [&](int kt, auto refill_tag) {
+    constexpr bool REFILL = decltype(refill_tag)::value && OTAMD_GEMM_ABL != 1;
     const char* ia = smem + stg * STAGE;
     const char* ib = ia + ABYTES;
     const int nstg = stg + 1 == NS ? 0 : stg + 1;
@@ -436,7 +490,9 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     // tile kt+1 has landed: the tiles after it that may still be in flight are kt+2 .. min(kt+NS-1, nk-1)
     wait_tiles(min(NS - 2, nk - kt - 2));
     if constexpr (OTAMD_GEMM_ABL != 4) BARRIER();
-    if (OTAMD_GEMM_ABL != 1 && kt + NS < nk) issue_tile(smem + stg * STAGE, kbeg + (kt + NS) * 64);   // refill tile kt's slot
+    if constexpr (REFILL && !SPREAD) {   // refill tile kt's slot
+      if (kt + NS < nk) issue_tile(smem + stg * STAGE, kbeg + (kt + NS) * 64);
+    }
     if constexpr (CS) {   // tile kt+1: published by this barrier, refilled only after the next one
       __builtin_amdgcn_sched_barrier(0);
       if (cs_on && kt + 1 < nk) colsum_tile(smem + nstg * STAGE);
@@ -446,14 +502,25 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
       const char* na = smem + nstg * STAGE;
       if constexpr (OTAMD_GEMM_ABL != 3) {
-        load_b(fb0, na + ABYTES, 0);
-        load_a(fa0, na, 0);
+        if constexpr (REFILL && SPREAD) load_ab_refill(fa0, fb0, na, na + ABYTES, smem + stg * STAGE, kbeg + (kt + NS) * 64);
+        else {
+          load_b(fb0, na + ABYTES, 0);
+          load_a(fa0, na, 0);
+        }
       }
       mfma_block(fa1, fb1);
       if constexpr (OTAMD_GEMM_ABL != 3) interleave();
     }
     __builtin_amdgcn_sched_barrier(0);
     stg = nstg;
+  };
+  if constexpr (SPREAD) {
+    int kt = 0;
+    for (; kt < nk - NS; ++kt) kstep(kt, std::true_type{});
+    for (; kt < nk; ++kt) kstep(kt, std::false_type{});
+  } else {   // conv gathers / the LoRA second segment: one body, the refill as a burst behind a uniform branch (a
+             // peeled copy measured 4-8 % slower on the conv tiles)
+    for (int kt = 0; kt < nk; ++kt) kstep(kt, std::true_type{});
   }
 
   const bool use_slab = gridDim.z > 1;
