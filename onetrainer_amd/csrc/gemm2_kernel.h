@@ -107,16 +107,12 @@ struct Stage {
     if constexpr (KM) t0 = (lane & 7) ^ ((lane >> 3) & 7);
   }
 
-  // source byte offset of this wave's piece i of the K tile at k0, plain K / MN modes (no conv gather)
-  __device__ __forceinline__ unsigned offset(long long ld, int k0, int Kend, int i) const {
-    static_assert(MODE == OPM_K || MODE == OPM_MN, "plain operand modes");
-    if constexpr (MODE == OPM_K) {
-      const int k = k0 + 8 * t0;
-      return (k < Kend && ok[i]) ? (unsigned)(a[i] + k) * 2u : OFF_INVALID;
-    } else {
-      const int k = k0 + a[i];
-      return (ok[i] && k < Kend) ? (unsigned)(k * (int)ld + b[i]) * 2u : OFF_INVALID;
-    }
+  // source byte offset of this wave's piece i of the K tile at k0, any mode: offsets() for one piece; with i a compile-time index the other
+  // pieces' arithmetic is dead and dropped
+  __device__ __forceinline__ unsigned offset_g(const ConvGeom& g, long long ld, int k0, int Kend, int i) const {
+    unsigned tmp[NI];
+    offsets(g, ld, k0, Kend, tmp);
+    return tmp[i];
   }
   // this wave's piece i of the image at img (piece j = wave + NW i); absent pieces of an uneven image are skipped
   __device__ __forceinline__ void put(__amdgpu_buffer_rsrc_t rs, char* img, int wave, int i, unsigned off) const {
@@ -329,13 +325,17 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
   // at dst placed one after each read: the inline-asm DMA keeps its place among the DS reads (both touch memory)
   // while interleave()'s groups put the MFMAs between the reads
   constexpr int NIA = Stage<AM, BM, NW>::NI, NIB = Stage<BMODE, BN, NW>::NI;
-  constexpr bool SPREAD = !SEG2 && NW == 8 && (AM == OPM_K || AM == OPM_MN) && (BMODE == OPM_K || BMODE == OPM_MN);
+  // plain K / MN operands only: with a conv gather the per-piece offset arithmetic (integer divisions) inside phase B
+  // cost more than the burst (conv fwd / dgrad 10-15 % slower, profiles/r4_gemm_spread_conv_*), and the 128-row
+  // colsum tiles (at their 128-VGPR cap) spilled 15 registers
+  constexpr bool SPREAD = !SEG2 && NW == 8 && !(CS && BM == 128) && (AM == OPM_K || AM == OPM_MN) &&
+                          (BMODE == OPM_K || BMODE == OPM_MN);
   auto load_ab_refill = [&](bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ], const char* ia, const char* ib, char* dst, int k0) {
     if constexpr (SPREAD) {
       auto piece = [&](int t) {   // offsets computed at the piece (no per-step offset arrays: the 256-wide tiles sit
                                   // at the 256-VGPR cap)
-        if (t < NIA) sa.put(ra, dst, wave, t, sa.offset(args.lda, k0, kend, t));
-        else if (t < NIA + NIB) sb.put(rb, dst + ABYTES, wave, t - NIA, sb.offset(args.ldb, k0, kend, t - NIA));
+        if (t < NIA) sa.put(ra, dst, wave, t, sa.offset_g(args.ga, args.lda, k0, kend, t));
+        else if (t < NIA + NIB) sb.put(rb, dst + ABYTES, wave, t - NIA, sb.offset_g(args.gb, args.ldb, k0, kend, t - NIA));
       };
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
