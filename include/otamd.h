@@ -365,17 +365,18 @@ int otamd_adamw_bf16_range(void* p, const void* g, void* m, void* v, long long b
 int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups, int
     n_groups, const float* clip_coef, hipStream_t stream);
 
-/* replaces: nn.utils.clip_grad_norm_(parameters, clip_grad_norm) (modules/trainer/GenericTrainer.py:712-713) */
-int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void* chunks, int n_chunks, double*
-    tensor_sq, int n_tensors, float max_norm, float* out, hipStream_t stream);
+/* replaces: nn.utils.clip_grad_norm_(parameters, clip_grad_norm) (modules/trainer/GenericTrainer.py:712-713);
+   chunk_sq: double[n_chunks] scratch (one slot per chunk, summed per tensor in chunk order: deterministic) */
+int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void* chunks, int n_chunks, double* chunk_sq,
+    double* tensor_sq, int n_tensors, float max_norm, float* out, hipStream_t stream);
 
-/* replaces: clip_grad_norm_ split over the backward (GenericTrainer.py:712-713): per-tensor squared norms of the
-   chunks [c_begin, c_end) accumulated into tensor_sq (zeroed once per step by the caller) as soon as their
-   gradients are final, then the coefficient from the sums (out[0] coefficient, out[1] total norm) */
+/* replaces: clip_grad_norm_ split over the backward (GenericTrainer.py:712-713): squared norms of the chunks
+   [c_begin, c_end) into their slots chunk_sq[c] as soon as their gradients are final (every chunk once per step),
+   then the per-tensor sums in chunk order and the coefficient (out[0] coefficient, out[1] total norm) */
 int otamd_grad_sqnorm_chunks(const void* grads, int grad_dtype, const void* chunks, int c_begin, int c_end,
-                             double* tensor_sq, hipStream_t stream);
-int otamd_grad_clip_finalize(const double* tensor_sq, int n_tensors, float max_norm, int grad_dtype, float* out,
-                             hipStream_t stream);
+                             double* chunk_sq, hipStream_t stream);
+int otamd_grad_clip_finalize(const void* chunks, int n_chunks, const double* chunk_sq, double* tensor_sq,
+                             int n_tensors, float max_norm, int grad_dtype, float* out, hipStream_t stream);
 
 /* replaces: the grad scaling half of clip_grad_norm_ when not fused into AdamW */
 int otamd_scale_bf16_by_device_scalar(void* g, long long n, const float* coef, hipStream_t stream);

@@ -89,9 +89,9 @@ SIGNATURES: dict[str, list] = {
     "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_bf16_range": [VP, VP, VP, VP, LL, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],
-    "otamd_grad_clip_coef": [VP, I, VP, I, VP, I, F, VP, VP],
+    "otamd_grad_clip_coef": [VP, I, VP, I, VP, VP, I, F, VP, VP],
     "otamd_grad_sqnorm_chunks": [VP, I, VP, I, I, VP, VP],
-    "otamd_grad_clip_finalize": [VP, I, F, I, VP, VP],
+    "otamd_grad_clip_finalize": [VP, I, VP, VP, I, F, I, VP, VP],
     "otamd_scale_bf16_by_device_scalar": [VP, LL, VP, VP],
     # norm.hip
     "otamd_groupnorm_fwd": [VP, LL, VP, LL, I, I, I, I, F, VP, VP, I, VP, VP, VP, VP, VP, VP],

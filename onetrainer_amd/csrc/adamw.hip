@@ -251,9 +251,12 @@ __device__ __forceinline__ float ld_as_f(const T* p, long long i);
 template <> __device__ __forceinline__ float ld_as_f<bf16_t>(const bf16_t* p, long long i) { return bf2f(p[i]); }
 template <> __device__ __forceinline__ float ld_as_f<float>(const float* p, long long i) { return p[i]; }
 
+// chunk_sq[blockIdx.x] = the chunk's sum of squares (one slot per chunk: no atomics, so the per-tensor sums below
+// add the chunks in a fixed order -- a double atomicAdd per chunk made the sum's last bits, and now and then the
+// bf16-rounded clip coefficient, depend on the chunks' arrival order)
 template <typename T>
 __global__ void __launch_bounds__(256) grad_sqnorm_kernel(const T* __restrict__ G, const NormChunk* __restrict__ chunks,
-                                                          double* __restrict__ tensor_sq) {
+                                                          double* __restrict__ chunk_sq) {
   const NormChunk c = chunks[blockIdx.x];
   double acc = 0.0;
   // 16-byte vector body (chunk bounds are multiples of 8 elements)
@@ -277,7 +280,21 @@ __global__ void __launch_bounds__(256) grad_sqnorm_kernel(const T* __restrict__ 
   acc = wave_sum_d(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(&tensor_sq[c.tensor], red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) chunk_sq[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// tensor_sq[t] = sum of tensor t's chunk slots in chunk order (the chunk table lists each tensor's chunks
+// contiguously, in element order); the thread of a tensor's first chunk walks them.  Tensors without chunks keep
+// the zero the caller's memset left.
+__global__ void tensor_sq_kernel(const NormChunk* __restrict__ chunks, int n_chunks, const double* __restrict__ chunk_sq,
+                                 double* __restrict__ tensor_sq) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n_chunks; c += gridDim.x * blockDim.x) {
+    const int t = chunks[c].tensor;
+    if (c > 0 && chunks[c - 1].tensor == t) continue;
+    double s = 0.0;
+    for (int k = c; k < n_chunks && chunks[k].tensor == t; ++k) s += chunk_sq[k];
+    tensor_sq[t] = s;
+  }
 }
 
 // total_norm / clip coefficient with torch's bf16 result dtypes:
@@ -378,42 +395,51 @@ OTAMD_API int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long lon
 }
 
 // grads: flat store (bf16 if grad_dtype==0 else f32); chunks: device table of n_chunks NormChunk;
-// tensor_sq: device double[n_tensors] (zeroed here); out: device float[2] = {clip coef, total norm}
-OTAMD_API int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void* chunks, int n_chunks,
+OTAMD_API int otamd_grad_clip_finalize(const void* chunks, int n_chunks, const double* chunk_sq, double* tensor_sq,
+                                       int n_tensors, float max_norm, int grad_dtype, float* out, hipStream_t stream);
+
+// chunk_sq: device double[n_chunks] scratch; tensor_sq: device double[n_tensors] (zeroed here); out: device
+// float[2] = {clip coef, total norm}
+OTAMD_API int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void* chunks, int n_chunks, double* chunk_sq,
                                    double* tensor_sq, int n_tensors, float max_norm, float* out, hipStream_t stream) {
-  if (!grads || !chunks || !tensor_sq || !out || n_chunks < 0 || n_tensors < 1) return OTAMD_EINVAL;
-  if (hipMemsetAsync(tensor_sq, 0, sizeof(double) * n_tensors, stream) != hipSuccess) return OTAMD_ELAUNCH;
+  if (!grads || !chunks || !tensor_sq || !out || n_chunks < 0 || n_tensors < 1 || (n_chunks > 0 && !chunk_sq))
+    return OTAMD_EINVAL;
   if (n_chunks > 0) {
     if (grad_dtype == 0)
-      grad_sqnorm_kernel<bf16_t><<<n_chunks, 256, 0, stream>>>((const bf16_t*)grads, (const NormChunk*)chunks, tensor_sq);
+      grad_sqnorm_kernel<bf16_t><<<n_chunks, 256, 0, stream>>>((const bf16_t*)grads, (const NormChunk*)chunks, chunk_sq);
     else
-      grad_sqnorm_kernel<float><<<n_chunks, 256, 0, stream>>>((const float*)grads, (const NormChunk*)chunks, tensor_sq);
+      grad_sqnorm_kernel<float><<<n_chunks, 256, 0, stream>>>((const float*)grads, (const NormChunk*)chunks, chunk_sq);
     OTAMD_CHECK_LAUNCH();
   }
-  clip_coef_kernel<<<1, 1024, 0, stream>>>(tensor_sq, n_tensors, max_norm, grad_dtype == 0, out);
-  OTAMD_CHECK_LAUNCH();
-  return OTAMD_OK;
+  return otamd_grad_clip_finalize(chunks, n_chunks, chunk_sq, tensor_sq, n_tensors, max_norm, grad_dtype, out, stream);
 }
 
-// the grad-norm pass split over the backward (util/optimizer/adamw_fused.OverlappedGradNorm): the per-tensor
-// squared norms of chunks [c_begin, c_end) accumulated into tensor_sq (zeroed by the caller once per step) as
-// soon as those tensors' gradients are final, on the weight-gradient stream beside the dgrad chain ...
+// the grad-norm pass split over the backward (util/optimizer/adamw_fused.OverlappedGradNorm): the squared norms of
+// chunks [c_begin, c_end) into their slots chunk_sq[c] as soon as those tensors' gradients are final, on the
+// weight-gradient stream beside the dgrad chain ...
 OTAMD_API int otamd_grad_sqnorm_chunks(const void* grads, int grad_dtype, const void* chunks, int c_begin, int c_end,
-                                       double* tensor_sq, hipStream_t stream) {
-  if (!grads || !chunks || !tensor_sq || c_begin < 0 || c_end < c_begin) return OTAMD_EINVAL;
+                                       double* chunk_sq, hipStream_t stream) {
+  if (!grads || !chunks || !chunk_sq || c_begin < 0 || c_end < c_begin) return OTAMD_EINVAL;
   if (c_end == c_begin) return OTAMD_OK;
   const NormChunk* c = (const NormChunk*)chunks + c_begin;
-  if (grad_dtype == 0) grad_sqnorm_kernel<bf16_t><<<c_end - c_begin, 256, 0, stream>>>((const bf16_t*)grads, c, tensor_sq);
-  else grad_sqnorm_kernel<float><<<c_end - c_begin, 256, 0, stream>>>((const float*)grads, c, tensor_sq);
+  if (grad_dtype == 0)
+    grad_sqnorm_kernel<bf16_t><<<c_end - c_begin, 256, 0, stream>>>((const bf16_t*)grads, c, chunk_sq + c_begin);
+  else
+    grad_sqnorm_kernel<float><<<c_end - c_begin, 256, 0, stream>>>((const float*)grads, c, chunk_sq + c_begin);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
 
-// ... and the clip coefficient from the accumulated per-tensor sums (clip_grad_norm_'s torch dtypes, as
-// otamd_grad_clip_coef)
-OTAMD_API int otamd_grad_clip_finalize(const double* tensor_sq, int n_tensors, float max_norm, int grad_dtype,
-                                       float* out, hipStream_t stream) {
-  if (!tensor_sq || !out || n_tensors < 1) return OTAMD_EINVAL;
+// ... and the clip coefficient: per-tensor sums of the chunk slots in chunk order, then clip_grad_norm_'s torch
+// dtypes (as otamd_grad_clip_coef)
+OTAMD_API int otamd_grad_clip_finalize(const void* chunks, int n_chunks, const double* chunk_sq, double* tensor_sq,
+                                       int n_tensors, float max_norm, int grad_dtype, float* out, hipStream_t stream) {
+  if (!chunks || !tensor_sq || !out || n_tensors < 1 || n_chunks < 0 || (n_chunks > 0 && !chunk_sq)) return OTAMD_EINVAL;
+  if (hipMemsetAsync(tensor_sq, 0, sizeof(double) * n_tensors, stream) != hipSuccess) return OTAMD_ELAUNCH;
+  if (n_chunks > 0) {
+    tensor_sq_kernel<<<(n_chunks + 255) / 256, 256, 0, stream>>>((const NormChunk*)chunks, n_chunks, chunk_sq, tensor_sq);
+    OTAMD_CHECK_LAUNCH();
+  }
   clip_coef_kernel<<<1, 1024, 0, stream>>>(tensor_sq, n_tensors, max_norm, grad_dtype == 0, out);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;

@@ -1159,7 +1159,8 @@ static int attn_bwd_impl(const AttnArgs* in, float* ws, long long ws_bytes, floa
     launch(attn_bwd_dq_kernel<64, 3>, gq, 3 * 2 * KT * 64 * 2, stream, a);
     launch(attn_bwd_dkv_kernel<64, 3, 64>, gk, dkv_lds<64, 64>(), stream, a);
   } else {
-    launch(attn_bwd_dq_kernel<128, 3, 32>, gq, 3 * 2 * 32 * 128 * 2, stream, a);   // 1349 vs 1467 us (64-key tiles)
+    // 64-key tiles 2 deep: 1086 vs 1104 us for 32-key tiles 3 deep (Flux 4x2381x24, round 4, same box)
+    launch(attn_bwd_dq_kernel<128, 2, 64>, gq, 2 * 2 * 64 * 128 * 2, stream, a);
     launch(attn_bwd_dkv_kernel<128, 1, 64>, gk, dkv_lds<128, 64>(), stream, a);
   }
   OTAMD_CHECK_LAUNCH();

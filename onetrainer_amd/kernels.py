@@ -589,12 +589,14 @@ def adamw_f32(p, g, m, v, groups, clip_coef=None):
           "otamd_adamw_f32")
 
 
-def grad_clip_coef(grads, chunks_dev, n_chunks, tensor_sq, n_tensors, max_norm, out):
+def grad_clip_coef(grads, chunks_dev, n_chunks, chunk_sq, tensor_sq, n_tensors, max_norm, out):
     _req(grads.dtype in (BF16, F32) and grads.is_contiguous(), "grads flat")
+    _req(chunk_sq.dtype == torch.float64 and chunk_sq.numel() >= n_chunks, "chunk_sq f64")
     _req(tensor_sq.dtype == torch.float64 and tensor_sq.numel() >= n_tensors, "tensor_sq f64")
     _req(out.dtype == F32 and out.numel() >= 2, "out f32[2]")
     check(lib().otamd_grad_clip_coef(_p(grads), 0 if grads.dtype == BF16 else 1, _p(chunks_dev), n_chunks,
-                                     _p(tensor_sq), n_tensors, float(max_norm), _p(out), stream_handle()),
+                                     _p(chunk_sq), _p(tensor_sq), n_tensors, float(max_norm), _p(out),
+                                     stream_handle()),
           "otamd_grad_clip_coef")
 
 

@@ -70,6 +70,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self._chunks = raw.to(store.device)
         self._n_chunks = len(chunks)
         self._tensor_sq = torch.zeros(len(store.order), dtype=torch.float64, device=store.device)
+        self._chunk_sq = torch.zeros(max(1, len(chunks)), dtype=torch.float64, device=store.device)   # one slot per chunk
         self.clip_out = torch.zeros(2, dtype=torch.float32, device=store.device)   # [coef, total norm]
         self._chunk_tensor = [c[2] for c in chunks]
         self.norm_overlap = None   # OverlappedGradNorm, attached by the trainer (single process, clip on)
@@ -96,13 +97,15 @@ class FusedAdamW(torch.optim.Optimizer):
         self.store.wait_params()   # the previous (overlapped) update still reads grads / clip_out
         nt = len(self.store.order)
         if self.norm_overlap is not None and self.norm_overlap.take():   # sums accumulated during backward
-            _lib.check(_lib.lib().otamd_grad_clip_finalize(self._tensor_sq.data_ptr(), nt, float(max_norm),
+            _lib.check(_lib.lib().otamd_grad_clip_finalize(self._chunks.data_ptr(), self._n_chunks,
+                                                           self._chunk_sq.data_ptr(), self._tensor_sq.data_ptr(), nt,
+                                                           float(max_norm),
                                                            0 if self.store.grad.dtype == torch.bfloat16 else 1,
                                                            self.clip_out.data_ptr(), K.stream_handle()),
                        "otamd_grad_clip_finalize")
         else:
-            K.grad_clip_coef(self.store.grad, self._chunks, self._n_chunks, self._tensor_sq, nt, max_norm,
-                             self.clip_out)
+            K.grad_clip_coef(self.store.grad, self._chunks, self._n_chunks, self._chunk_sq, self._tensor_sq, nt,
+                             max_norm, self.clip_out)
         self._pending_clip = True
         return self.clip_out[1]
 
@@ -231,9 +234,10 @@ class OverlappedGradNorm:
     `bucket_bytes` (whole tensors, reverse layout order = the order backward finishes them) are summed on the
     weight-gradient stream as soon as every tensor in the range has its gradient -- the stream then waits for
     the dgrad chain's position, so both streams' writes are ordered before the read.  clip_grad_norm_ then only
-    folds the per-tensor sums (otamd_grad_clip_finalize) instead of reading the whole gradient buffer (SDXL:
-    5.1 GB, ~0.9 ms) after backward.  The per-tensor sums are fp64 and the coefficient is formed with torch's
-    bf16 roundings exactly as otamd_grad_clip_coef does.  Ranges with a tensor that received no gradient are
+    folds the per-chunk sums into per-tensor ones in chunk order (otamd_grad_clip_finalize) instead of reading
+    the whole gradient buffer (SDXL: 5.1 GB, ~0.9 ms) after backward.  The sums are fp64, one slot per chunk
+    (no atomics: the same bits every run), and the coefficient is formed with torch's bf16 roundings exactly as
+    otamd_grad_clip_coef does.  Ranges with a tensor that received no gradient are
     summed after finish_backward has zeroed it.  OTAMD_NORM_OVERLAP=0 disables it."""
 
     def __init__(self, opt: FusedAdamW, bucket_bytes: int = 64 << 20):
@@ -273,9 +277,7 @@ class OverlappedGradNorm:
         self.armed = update_step
         self.ready = False
         self.pending = [len(b[2]) for b in self.buckets]
-        self.launched = [False] * len(self.buckets)
-        if update_step:
-            self.opt._tensor_sq.zero_()
+        self.launched = [False] * len(self.buckets)   # every bucket's chunk slots are rewritten each armed step
 
     def _launch(self, bi, side):
         self.launched[bi] = True
@@ -290,11 +292,11 @@ class OverlappedGradNorm:
             side.wait_event(self._ev)
             with torch.cuda.stream(side):
                 _lib.check(_lib.lib().otamd_grad_sqnorm_chunks(g.data_ptr(), dtype, opt._chunks.data_ptr(), c0, c1,
-                                                               opt._tensor_sq.data_ptr(), K.stream_handle()),
+                                                               opt._chunk_sq.data_ptr(), K.stream_handle()),
                            "otamd_grad_sqnorm_chunks")
         else:
             _lib.check(_lib.lib().otamd_grad_sqnorm_chunks(g.data_ptr(), dtype, opt._chunks.data_ptr(), c0, c1,
-                                                           opt._tensor_sq.data_ptr(), K.stream_handle()),
+                                                           opt._chunk_sq.data_ptr(), K.stream_handle()),
                        "otamd_grad_sqnorm_chunks")
 
     def _on_ready(self, names):
