@@ -139,7 +139,8 @@ def _tune(a: GemmArgs, device) -> tuple:
 # as data: deterministic plans (the same split-K summation order in every process, so resume stays
 # bit-exact), measured rather than modelled.  Signatures not in the table use the analytic plan.
 # OTAMD_GEMM_TABLE=0 disables it (A/B against the analytic planner).
-_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plans_mi355x.json")
+_TABLE_PATH = (os.environ.get("OTAMD_GEMM_TABLE_PATH")   # another table for A/B measurements
+               or os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plans_mi355x.json"))
 _PLAN_TABLE = None
 
 
