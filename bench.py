@@ -153,6 +153,14 @@ def pmc_traffic(model: str):
         return path, json.load(f)
 
 
+def _die_with_parent():
+    """child side of launch_ranks, before exec: SIGTERM when the launcher dies (a launcher killed by a timeout
+    must not leave ranks running on the GPU)"""
+    import ctypes
+    import signal
+    ctypes.CDLL(None).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
+
+
 def launch_ranks(n: int) -> int:
     """`bench.py --gpus N` without a torchrun environment: start N fresh child ranks (one per GPU,
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env) before this process touches the GPU, wait
@@ -167,7 +175,8 @@ def launch_ranks(n: int) -> int:
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      preexec_fn=_die_with_parent))
     import time
     while True:   # a rank that fails ends the others (its peers would otherwise block in their next collective)
         rcs = [p.poll() for p in procs]
