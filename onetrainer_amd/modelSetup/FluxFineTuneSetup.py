@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import torch
 
+from ..util.dtype_util import dtype_plan
 from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
 from ..util.optimizer.adamw_fused import FusedAdamW
 from ..util.optimizer_util import restore_training_state
@@ -24,6 +25,7 @@ class FluxFineTuneSetup(BaseFluxSetup):
 
     def setup_optimizations(self, model, config):
         config = plain(config)
+        model.dtype_plan = dtype_plan(config)   # util/dtype_util.py: the config's dtypes honoured, overridden or refused
         model.train_dtype = torch.bfloat16
 
     def setup_model(self, model, config):

@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import torch
 
+from ..util.dtype_util import dtype_plan
 from ..module.lora import LoRAWrapper
 from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
 from ..util.optimizer.adamw_fused import FusedAdamW
@@ -36,6 +37,7 @@ class FluxLoRASetup(BaseFluxSetup):
 
     def setup_optimizations(self, model, config):
         config = plain(config)
+        model.dtype_plan = dtype_plan(config)   # util/dtype_util.py: the config's dtypes honoured, overridden or refused
         model.train_dtype = torch.bfloat16
 
     def setup_model(self, model, config):

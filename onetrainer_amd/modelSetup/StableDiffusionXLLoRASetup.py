@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import torch
 
+from ..util.dtype_util import dtype_plan
 from ..module.lora import PRESETS, LoRAUNetWrapper
 from ..util.NamedParameterGroup import NamedParameterGroup, NamedParameterGroupCollection
 from ..util.optimizer.adamw_fused import FusedAdamW
@@ -28,6 +29,7 @@ class StableDiffusionXLLoRASetup(BaseStableDiffusionXLSetup):
 
     def setup_optimizations(self, model, config):
         config = plain(config)
+        model.dtype_plan = dtype_plan(config)   # util/dtype_util.py: the config's dtypes honoured, overridden or refused
         model.train_dtype = torch.bfloat16
 
     @staticmethod

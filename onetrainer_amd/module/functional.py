@@ -498,6 +498,7 @@ class CrossAttnFn(torch.autograd.Function):
                    cast_stream=side)
         if side is not None:
             dkv.record_stream(side)
+            S.note_side((dkv,))
         return dq, (dkv if ctx.needs_input_grad[1] else None), None, None
 
 

@@ -29,6 +29,7 @@ _ENABLED = os.environ.get("OTAMD_WGRAD_STREAM", "1") != "0"
 _AVAIL = None
 _STREAMS: dict = {}   # raw HIP stream -> torch Stream object (current_stream() builds a new one per call)
 _EVENTS: dict = {}    # side stream index -> reusable fork event (a wait captures the record current at enqueue)
+_HAZARD: list = []    # active module/stream_hazards.StreamHazardCheck instances (debug / tests only)
 
 
 def enabled() -> bool:
@@ -85,6 +86,18 @@ def wgrad_region(tensors=()):
     for t in tensors:
         if t is not None and t.is_cuda:
             t.record_stream(side)
+    if _HAZARD:
+        note_side(tensors, 3)
+
+
+def note_side(tensors, depth: int = 1):
+    """tell an active hazard checker that the side stream may read these tensors until the next join()"""
+    if _HAZARD:
+        import sys
+        fr = sys._getframe(depth)
+        label = f"{fr.f_code.co_filename.rsplit('/', 1)[-1]}:{fr.f_lineno}"
+        for h in _HAZARD:
+            h.side_read(tensors, label)
 
 
 def join():
@@ -92,6 +105,8 @@ def join():
     side = side_stream()
     if side is not None:
         torch.cuda.current_stream().wait_stream(side)
+    for h in _HAZARD:
+        h.joined()
 
 
 def after_side(fn):

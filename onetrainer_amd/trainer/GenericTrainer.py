@@ -77,6 +77,9 @@ class GenericTrainer(TimedActionMixin):
             self.model_setup = create.create_model_setup(cfg, self.device, self.rank, self.world)
         self.model_setup.setup_model(self.model, cfg)
         self.model_setup.setup_train_device(self.model, cfg)
+        plan = getattr(self.model, "dtype_plan", None)
+        if plan is not None and plan.overrides and self.rank == 0:   # util/dtype_util.py: recorded, not silent
+            print(f"dtype policy: {plan.summary()}", flush=True)
         self.parameters = self.model.parameters.parameters()
         if self.world > 1:
             self.reducer = GradBucketReducer(self.model.train_store, bucket_bytes=cfg.dp_bucket_mb << 20,

@@ -41,7 +41,11 @@ class TrainConfig:
     training_method: str = "FINE_TUNE"
     train_device: str = "cuda"
     temp_device: str = "cpu"
+    # the build trains bf16 (util/dtype_util.py); the reference's defaults are FLOAT_16 / FLOAT_32
+    # (TrainConfig.py:782,816), which util/dtype_util.dtype_plan overrides or refuses with a recorded reason
     train_dtype: str = "BFLOAT_16"
+    fallback_train_dtype: str = "BFLOAT_16"
+    enable_autocast_cache: bool = True
     weight_dtype: str = "BFLOAT_16"
     resolution: str = "1024"
     batch_size: int = 1
@@ -121,7 +125,18 @@ class TrainConfig:
 
     @staticmethod
     def default_values() -> "TrainConfig":
+        """the build's defaults: bf16 weights and bf16 compute (what SURVEY.md §8(d)'s C2-C5 configure)"""
         return TrainConfig()
+
+    @staticmethod
+    def reference_defaults() -> "TrainConfig":
+        """the reference's TrainConfig.default_values() for the fields where the build's defaults differ
+        (TrainConfig.py:782,816-817: weight_dtype FLOAT_32, train_dtype FLOAT_16): the starting point of a
+        reference JSON config (scripts/train.py), so a preset that leaves a dtype unset gets the reference's
+        value and util/dtype_util.dtype_plan records or refuses what the build does with it"""
+        c = TrainConfig()
+        c.weight_dtype, c.train_dtype, c.fallback_train_dtype = "FLOAT_32", "FLOAT_16", "BFLOAT_16"
+        return c
 
     def from_dict(self, d: dict) -> "TrainConfig":
         names = {f.name: f for f in fields(self)}

@@ -20,14 +20,18 @@ def is_flux(model_type: str) -> bool:
 def create_model(config, device, seed=0, unet_config=None, prediction_type="epsilon", flux_config=None):
     """random-weight model of the configured architecture (weights from disk: SURVEY.md §8(f) #2).
     LoRA training keeps the base network frozen (no gradient buffer)."""
+    from .dtype_util import dtype_plan
     config = plain(config)
+    plan = dtype_plan(config)   # ValueError for a dtype setup the build cannot train, before any allocation
     mt = config.model_type
     if is_flux(mt):
         from ..model.FluxModel import FluxModel
         from ..module import flux as FX
         tr = FX.FluxTransformer2DModel(flux_config or FX.flux_dev_config(), device, seed=seed,
                                        trainable=config.training_method != "LORA")
-        return FluxModel(tr, model_type=mt)
+        m = FluxModel(tr, model_type=mt)
+        m.dtype_plan = plan
+        return m
     if unet_config is None:
         unet_config = _unet_config_on_disk(config)
     if unet_config is None:
@@ -39,7 +43,9 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
             raise NotImplementedError(f"model type {mt}")
     unet = U.UNet2DConditionModel(unet_config, device, seed=seed, trainable=config.training_method != "LORA")
     ns = NoiseScheduler(device, prediction_type=prediction_type)
-    return StableDiffusionXLModel(unet, ns, SCALING.get(mt, 0.13025), model_type=mt)
+    m = StableDiffusionXLModel(unet, ns, SCALING.get(mt, 0.13025), model_type=mt)
+    m.dtype_plan = plan
+    return m
 
 
 def _unet_config_on_disk(config):

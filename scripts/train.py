@@ -39,17 +39,25 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def load_config(path: str):
+    """TrainConfig.default_values().from_dict(json) as scripts/train.py:23-25 does, from the reference's defaults
+    (TrainConfig.reference_defaults): fields a JSON leaves unset take the reference's values, and the dtype policy
+    (util/dtype_util.dtype_plan) records or refuses what this build does with them"""
+    from onetrainer_amd.util.config.TrainConfig import TrainConfig
+    train_config = TrainConfig.reference_defaults()
+    with open(path, "r") as f:
+        train_config.from_dict(json.load(f))
+    return train_config
+
+
 def main(argv=None):
     args = parse_args(argv)
     from onetrainer_amd.trainer.GenericTrainer import GenericTrainer
     from onetrainer_amd.util.TrainCommands import TrainCommands
-    from onetrainer_amd.util.config.TrainConfig import TrainConfig
 
     callbacks = TrainCallbacks()
     commands = TrainCommands()
-    train_config = TrainConfig.default_values()
-    with open(args.config_path, "r") as f:
-        train_config.from_dict(json.load(f))
+    train_config = load_config(args.config_path)
     try:   # secrets (hub tokens, cloud keys) are not used by this build; a named file must exist
         with open("secrets.json" if args.secrets_path is None else args.secrets_path, "r") as f:
             train_config.extra["secrets"] = json.load(f)

@@ -39,6 +39,7 @@ def test_train_script_runs_reference_config(dev, tmp_path):
     cfg = {"__version": 6, "model_type": "STABLE_DIFFUSION_15", "training_method": "FINE_TUNE",
            "cache_dir": str(cache), "batch_size": 2, "epochs": 1, "learning_rate": 1e-5,
            "learning_rate_warmup_steps": 0, "workspace_dir": str(tmp_path / "ws"), "train_dtype": "BFLOAT_16",
+           "weight_dtype": "BFLOAT_16",
            "optimizer": {"optimizer": "ADAMW", "stochastic_rounding": True},
            "unet": {"train": True}, "text_encoder": {"train": False}, "base_model_name": str(tmp_path / "base"),
            "output_model_destination": str(tmp_path / "out" / "model.safetensors"), "output_model_format": "SAFETENSORS",
