@@ -480,10 +480,12 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
 
 // dQ: per wave 32 queries, iterate over key tiles (a dual-use K image -- row reads for S, transposed reads for
 // dQ -- and a V image per stage)
-// NS = LDS ring depth, KTD = keys per tile.  D = 128 runs 32-key tiles 3 deep (72 KiB): two blocks
-// per CU (the 64-key 3-deep ring, 144 KiB, left one block -- one wave per SIMD).  D = 64 with NS = 2 (48 KiB) lets three blocks share a CU (150 VGPRs fit three
-// waves per SIMD), so the SDXL level-2 grid (8 x 20 heads x 4 = 640 blocks) runs in one round of
-// 768 slots instead of 1.25 rounds of 512 with NS = 3 (72 KiB).
+// NS = LDS ring depth, KTD = keys per tile.  Launched as (otamd_attn_bwd):
+//   D = 64:  <64, 3> -- 32-key tiles 3 deep (24 KiB: one dual-use K image and one V image per stage); three
+//            blocks per CU (__launch_bounds__(256, 3), set by the VGPRs), so the SDXL level-2 grid
+//            (8 x 20 heads x 4 = 640 blocks) runs in one round of 768 slots
+//   D = 128: <128, 2, 64> -- 64-key tiles 2 deep (64 KiB), two blocks per CU: 1086 us per Flux call
+//            (4 x 2381 x 24 heads) against 1104 us for 32-key tiles 3 deep (round 4, same box)
 template <int D, int NS, int KTD = KT>
 __global__ void __launch_bounds__(256, D == 64 ? 3 : 2) attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1167,7 +1169,11 @@ static int attn_bwd_impl(const AttnArgs* in, float* ws, long long ws_bytes, floa
   if (qsplit > 1) {
     hipStream_t cs = stream;
     if (slabs && cast_stream != stream) {   // the sum after the slabs' producer, on the other stream
-      thread_local hipEvent_t ev = nullptr;
+      // one fork event per (thread, device): an event records only on streams of the device it was created on
+      thread_local hipEvent_t evs[64] = {};
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return OTAMD_ELAUNCH;
+      hipEvent_t& ev = evs[dev];
       if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return OTAMD_ELAUNCH;
       if (hipEventRecord(ev, stream) != hipSuccess || hipStreamWaitEvent(cast_stream, ev, 0) != hipSuccess)
         return OTAMD_ELAUNCH;

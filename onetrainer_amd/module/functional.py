@@ -493,7 +493,11 @@ class CrossAttnFn(torch.autograd.Function):
         C = q.shape[-1]
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
-        side = S.side_stream() if (ctx.kv_wgrad_only and _CROSS_CAST_SIDE and ctx.needs_input_grad[1]) else None
+        # the side stream only when every reader of dkv is queued there: PrecomputedLinearFn's weight gradient reads
+        # dkv in place (rows of 2C elements, 16-byte aligned when C % 4 == 0; otherwise its main-stream
+        # .contiguous() copy would read dkv before the cast) and kv_wgrad_only says no dx (text states need none)
+        side = S.side_stream() if (ctx.kv_wgrad_only and _CROSS_CAST_SIDE and ctx.needs_input_grad[1]
+                                   and C % 4 == 0) else None
         K.attn_bwd(q, kv[..., :C], kv[..., C:], o, lse, do, ctx.heads, dq=dq, dk=dkv[..., :C], dv=dkv[..., C:],
                    cast_stream=side)
         if side is not None:

@@ -52,6 +52,7 @@ class GenericTrainer(TimedActionMixin):
         self.one_step_trained = False
         self._has_gradient = False
         self._wallclock_timers = False
+        self._det_flags = 0                # backup / save raised by STEP / EPOCH timers under DP (_raise_timed)
         self._ctl_group = None
         self.agreements = 0
         self.rank, self.world = 0, 1
@@ -283,15 +284,28 @@ class GenericTrainer(TimedActionMixin):
                 and self.repeating_action_needed("save", cfg.save_every, cfg.save_every_unit, tp, start_at_zero=False))
 
     agree_every = 16   # update steps between the ranks' backup / save agreements under wall-clock timers
+    WALLCLOCK = ("SECOND", "MINUTE", "HOUR")
 
     def _agreement_point(self, tp) -> bool:
-        """whether this (update-boundary) step consumes the backup / save commands.  Always in one process
-        or with only STEP / EPOCH timers (every rank raises the same commands at the same step); with a
-        wall-clock timer under data parallel only every `agree_every` update steps, where rank 0's decision
-        is broadcast (_agree), so the ranks do not meet on the host at every step."""
+        """whether this (update-boundary) step consumes the sticky backup / save commands.  Always in one process
+        or with only STEP / EPOCH timers; with a wall-clock timer under data parallel only every `agree_every`
+        update steps, where rank 0's decision is broadcast (_agree), so the ranks do not meet on the host at every
+        step.  Commands raised by a STEP / EPOCH timer under data parallel do not wait for this point (train():
+        every rank raises them at the same step, so they run at the exact step, as in the reference)."""
         if self.world == 1 or not self._wallclock_timers:
             return True
         return (tp.global_step // self.config.gradient_accumulation_steps) % self.agree_every == 0
+
+    def _raise_timed(self, kind: int, unit):
+        """a timer fired before this step (GenericTrainer.py:653-656): a command the next update boundary runs.
+        Under data parallel with wall-clock timers, STEP / EPOCH timers fire identically on every rank and are
+        kept apart from the sticky commands that need rank 0's decision."""
+        if self.world > 1 and self._wallclock_timers and TimedActionMixin._unit(unit) not in self.WALLCLOCK:
+            self._det_flags |= kind
+        elif kind == 1:
+            self.commands.backup()
+        else:
+            self.commands.save()
 
     def _agree(self, flags: int, step: int) -> int:
         """Ranks must take a backup / save together (both barrier).  A wall-clock timer can fire on one
@@ -321,6 +335,7 @@ class GenericTrainer(TimedActionMixin):
         # losses are read from the device every `flush_every` steps: printed when log_every is set, written as
         # the loss scalars either way (the reference logs them every update step, GenericTrainer.py:723-733)
         flush_every = log_every or 32
+        self._det_flags = 0
         frozen = False
         failed = True
         if self.tensorboard is None:
@@ -330,17 +345,11 @@ class GenericTrainer(TimedActionMixin):
                 self.data_loader.get_data_set().start_next_epoch()
                 for batch in self.data_loader.get_data_loader():
                     if self._needs_backup(tp):
-                        self.commands.backup()
+                        self._raise_timed(1, cfg.backup_after_unit)
                     if self._needs_save(tp):
-                        self.commands.save()
-                    if not self._has_gradient and self._agreement_point(tp):
-                        flags = (int(self.commands.get_and_reset_backup_command())
-                                 | int(self.commands.get_and_reset_save_command()) << 1)
-                        flags = self._agree(flags, tp.global_step)
-                        if flags & 1:
-                            self.backup(tp)
-                        if flags & 2:
-                            self.save(tp)
+                        self._raise_timed(2, cfg.save_every_unit)
+                    if not self._has_gradient:
+                        self._run_commands(tp, self._agreement_point(tp))
                     gs, update = tp.global_step, self._is_update_step(tp)
                     loss = self.train_step(batch)
                     self.loss_history.append(loss)
@@ -370,11 +379,29 @@ class GenericTrainer(TimedActionMixin):
         finally:
             if failed and self.world > 1:
                 self.abort_distributed()
-            elif not failed and steps % flush_every:
-                self._report_losses(steps % flush_every, echo=bool(log_every))   # the tail since the last flush
+            else:
+                if not failed and steps % flush_every:
+                    self._report_losses(steps % flush_every, echo=bool(log_every))   # the tail since the last flush
+                if not failed and self.world > 1 and self._wallclock_timers and not self._has_gradient:
+                    # a wall-clock command raised since the last agreement point: every rank ends the loop at the
+                    # same step, so one more agreement here runs it instead of dropping it
+                    self._run_commands(tp, True)
             if frozen:
                 gc.unfreeze()
             gc.enable()
+
+    def _run_commands(self, tp, agreement: bool):
+        """at an update boundary (no accumulated gradient pending): the backup / save the timers or the command
+        object asked for (GenericTrainer.py:653-668); sticky commands only at an agreement point"""
+        flags, self._det_flags = self._det_flags, 0
+        if agreement:
+            sticky = (int(self.commands.get_and_reset_backup_command())
+                      | int(self.commands.get_and_reset_save_command()) << 1)
+            flags |= self._agree(sticky, tp.global_step)
+        if flags & 1:
+            self.backup(tp)
+        if flags & 2:
+            self.save(tp)
 
     def abort_distributed(self):
         """a rank failed (exception, timed-out collective, KeyboardInterrupt) inside train(): abort the

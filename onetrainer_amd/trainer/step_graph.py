@@ -1,13 +1,11 @@
 """Whole-step HIP graph for the train step's forward + backward (MI355X-first: graphs instead of a
 tracing compiler; no reference counterpart -- the reference launches every op from Python).
 
-The SDXL step issues ~5,400 kernels (GEMM, attention, norm, elementwise) through autograd and
-ctypes: ~114 ms of host time per 146 ms step on MI355X.  A captured step is replayed with ONE host
-call.  OPT-IN (OTAMD_STEP_GRAPH=1): measured on MI355X / ROCm 7 (SDXL 1024^2 b=4, p50 ms):
-    eager + wgrad side stream 144.7 | eager, one stream 156.0 | graph, one stream 156.7 |
-    graph + side stream 160.9
-i.e. the host keeps ahead of the GPU (no gain from removing it) and the replayed graph does not
-keep the dgrad / wgrad stream overlap, so the eager two-stream step stays the default.
+OPT-IN (OTAMD_STEP_GRAPH=1).  The SDXL step issues ~4,000 kernels through autograd and the native host layer:
+71-77 ms of host time per ~133 ms GPU step.  A captured step replays with ONE host call (37 ms of host issue per
+step, round 4), but ran 145-147 ms on the GPU against 134 ms eager on the same box
+(profiles/r4_step_graph_and_fork_order.txt): the GPU, not the host, bounds the step today, so the eager
+two-stream step stays the default.
 
 What is captured and what stays eager (GenericTrainer.train_step):
   eager   noise + timesteps (Philox, seeded by global_step) into static buffers
@@ -23,8 +21,16 @@ happen there) and is captured on its second occurrence; all graphs share one mem
 never run concurrently).  Off when the step has host-varying inputs (text dropout masks), under
 gradient accumulation (the first micro-step overwrites gradients, later ones accumulate), and with
 data parallel (the bucket all-reduces are issued from inside backward; RCCL capture is not used).
-Results are bit-identical to the eager step
-(tests/test_train_step_gpu.py::test_step_graph_matches_eager).
+
+Correctness.  Under the runtime's default graph execution the replayed step is bit-identical to the eager step
+(tests/test_train_step_gpu.py::test_step_graph_matches_eager).  One round-4 run with the debug knob
+DEBUG_HIP_FORCE_GRAPH_QUEUES=2 ended on another loss (1.0354 vs 0.90086; the same knob on another box matched).
+Round 5 checked the two places such a race could come from: the captured graph has one root and one sink, with
+the weight-gradient branch joined into finish_backward (tests/test_stream_hazards_gpu.py, from
+hipGraphDebugDotPrint), and module/stream_hazards.StreamHazardCheck finds no main-stream access racing with the
+side stream in the SDXL, SD 1.5 and LoRA steps, at the aten layer and at every kernel entry point (and does find
+races planted on purpose).  The graph's edges therefore order every side-stream access the eager events order;
+the outlier is attributed to the runtime's multi-queue execution under that debug knob, which is not used.
 """
 from __future__ import annotations
 
@@ -81,6 +87,8 @@ class StepGraphs:
         store.finish_backward()
         return loss.detach()
 
+    debug_dot = None   # a path: capture in debug mode and write the graph's DOT there (tests, tools/graph_dump.py)
+
     def _capture(self, batch: dict) -> _Entry:
         tr = self.tr
         setup = tr.model_setup
@@ -92,7 +100,9 @@ class StepGraphs:
         e.timestep = torch.empty(shape[0], dtype=torch.int32, device=lat.device)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()   # the eager steps' cached blocks; the graph gets its own pool
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=bool(self.debug_dot))   # debug: keep the hipGraph_t for the dump
+        if self.debug_dot:
+            g.enable_debug_mode()
         setup.graph_inputs = (e.noise, e.timestep)
         try:
             with torch.cuda.graph(g, pool=self.pool):
@@ -101,6 +111,8 @@ class StepGraphs:
             setup.graph_inputs = None
         if self.pool is None:
             self.pool = g.pool()
+        if self.debug_dot:
+            g.debug_dump(self.debug_dot)
         e.graph = g
         return e
 

@@ -317,6 +317,8 @@ class OverlappedGradNorm:
         for bi in range(len(self.buckets)):
             if not self.launched[bi]:
                 self._launch(bi, None)
+        # every chunk slot is rewritten on an armed step: the finalize never sees an earlier step's sums
+        assert all(self.launched), "overlapped grad norm: a bucket was not summed this step"
         self.ready = True
 
     def take(self) -> bool:

@@ -183,7 +183,9 @@ def test_dead_peer_times_out_and_aborts():
 def _worker_wallclock(rank, world, port, q):
     """a MINUTE backup timer under data parallel: rank 0's wall clock fires, rank 1's does not; both ranks
     back up together, and the ranks meet on the host only every `agree_every` update steps (no per-step
-    rendezvous-store traffic, no keys left behind)."""
+    rendezvous-store traffic, no keys left behind).  A STEP save timer beside it saves at its exact steps (it
+    fires on every rank alike and does not wait for an agreement point), and the command rank 0 raised after
+    the last agreement point runs at the end of train() instead of being dropped."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank), OTAMD_DIST_BACKEND="gloo")
     from types import SimpleNamespace
@@ -199,6 +201,7 @@ def _worker_wallclock(rank, world, port, q):
         TM.time.time = lambda: now[0]
         cfg = TrainConfig.default_values()
         cfg.backup_after, cfg.backup_after_unit = 1, "MINUTE"
+        cfg.save_every, cfg.save_every_unit = 10, "STEP"
         cfg.workspace_dir = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"otamd_wallclock_{os.getpid()}")
         tp = TrainProgress()
         loader = SimpleNamespace(get_data_set=lambda: SimpleNamespace(start_next_epoch=lambda: None),
@@ -207,6 +210,8 @@ def _worker_wallclock(rank, world, port, q):
         tr.rank, tr.world = rank, world
         backups = []
         tr.backup = lambda t=None: backups.append(tp.global_step)
+        saves = []
+        tr.save = lambda t=None: saves.append(tp.global_step)
         store = dist.distributed_c10d._get_default_store()
         keys = {}
 
@@ -221,8 +226,9 @@ def _worker_wallclock(rank, world, port, q):
 
         tr.train_step = step
         tr.train(log_every=0, max_steps=40)
-        assert tr.agreements == 3, tr.agreements          # update steps 0, 16, 32
-        assert backups == [16, 32], backups
+        assert tr.agreements == 4, tr.agreements          # update steps 0, 16, 32 and the end of train()
+        assert backups == [16, 32, 40], backups
+        assert saves == [9, 19, 29, 39], saves         # the STEP timer's own steps (TimedActionMixin, pinned)
         assert store.num_keys() == keys[17], (store.num_keys(), keys)   # nothing written per step
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover

@@ -207,3 +207,34 @@ def test_grad_norm_deterministic(dev):
         assert torch.equal(t, runs[0][0]) and torch.equal(c, runs[0][1])
     want = torch.stack([st.params[n].grad.double().square().sum() for n, _ in shapes])
     assert torch.allclose(runs[0][0], want, rtol=1e-6, atol=0)   # 8-element fp32 partials, fp64 beyond
+
+
+def test_grad_norm_overlap_with_untouched_tensors(dev):
+    """OverlappedGradNorm when a step's backward leaves some tensors without a gradient: their buckets are summed in
+    finish() after finish_backward zeroed them, so the chunk slots of the previous step (poisoned here) never reach
+    the clip coefficient, which equals the end-of-step pass over the same gradients."""
+    from onetrainer_amd.util.optimizer.adamw_fused import OverlappedGradNorm
+    shapes = [(f"t{i}", (300 + 37 * i, 500)) for i in range(12)]
+    st = FlatParamStore([(n, s, "g") for n, s in shapes], torch.bfloat16, dev)
+    opt = FusedAdamW(st, [{"params": [st.params[n] for n, _ in shapes]}], lr=1e-3)
+    norm = OverlappedGradNorm(opt, bucket_bytes=1 << 20)
+    assert len(norm.buckets) > 4
+    g = torch.Generator(device="cpu").manual_seed(9)
+    touched = [n for i, (n, _) in enumerate(shapes) if i % 3 != 1]
+    opt._chunk_sq.fill_(1e9)                     # what a previous step left behind
+    norm.arm(True)
+    st.begin_backward()
+    for n, s in shapes:
+        if n in touched:
+            st.params[n].grad.copy_(torch.randn(s, generator=g) * 0.02)
+            st.mark_ready([n])
+    st.finish_backward()                        # zeroes the untouched tensors' gradients
+    norm.finish()
+    opt.norm_overlap = norm
+    total = opt.clip_grad_norm_(0.5).item()
+    coef = opt.clip_out[0].item()
+    opt.norm_overlap = None
+    total_ref = opt.clip_grad_norm_(0.5).item()
+    assert coef == opt.clip_out[0].item() and total == total_ref, (coef, total, total_ref)
+    want = torch.stack([st.params[n].grad.double().square().sum() for n, _ in shapes]).sum().sqrt().item()
+    assert abs(total - want) <= 1e-3 * want and total < 1e4
