@@ -209,6 +209,9 @@ def main():
                     help="sdxl: configs[2] per GPU (metric workload); sd15: configs[1] (SD 1.5 512^2 b=16); "
                          "flux: configs[4] per GPU (FLUX.1 LoRA r16, 768^2, b=4); sdxl-lora: configs[3] per GPU "
                          "(SDXL LoRA r32, aspect-ratio buckets drawn per step, b=4)")
+    ap.add_argument("--tiny", action="store_true",
+                    help="(tests of the bench's own legs, e.g. launch_ranks) the tiny SDXL-shaped test UNet instead of "
+                         "the full network; never a metric line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true", help="skip the VAE-encode (latent caching) side measurement")
     ap.add_argument("--autotune", action="store_true",
@@ -253,7 +256,21 @@ def main():
 
     from onetrainer_amd import kernels as K
     K.set_gemm_autotune(args.autotune)   # plans are tuned inside the untimed warm-up steps
-    tr = GenericTrainer(cfg)
+    tiny_kw = {}
+    if args.tiny:
+        from onetrainer_amd.module.unet import tiny_sdxl_config
+        from onetrainer_amd.util import create
+        if sd15 or flux or sdxl_lora:
+            raise SystemExit("--tiny: the sdxl workload only")
+        ucfg = tiny_sdxl_config()
+        tiny_kw = dict(te1_dim=48, te2_dim=48, pooled_dim=64)
+        args.no_cpu_baseline = args.no_vae = True
+        from onetrainer_amd.trainer import ddp
+        ddp.init_from_env()   # the model goes to this rank's device
+        tr = GenericTrainer(cfg, model=create.create_model(cfg, torch.device(f"cuda:{torch.cuda.current_device()}"),
+                                                            seed=0, unet_config=ucfg))
+    else:
+        tr = GenericTrainer(cfg)
     t0 = time.time()
     tr.start()
     rank, world = tr.rank, tr.world
@@ -274,7 +291,7 @@ def main():
         order = [random.Random(1000 + i).choice(buckets) for i in range(args.warmup + args.steps + 1)]
     else:
         batch = synthetic_sdxl_batch(args.batch, args.res, args.res, dev, seed=rank, sdxl=not sd15,
-                                     scaling_factor=0.18215 if sd15 else 0.13025)
+                                     scaling_factor=0.18215 if sd15 else 0.13025, **tiny_kw)
     if sdxl_lora:
         for r in buckets:   # every bucket shape once (plans, workspaces), untimed
             tr.train_step(arb[r])
@@ -364,6 +381,8 @@ def main():
         basis = f"{train_tf_img:.3f} TFLOP/image algorithmic (3 x {fwd_tf:.3f} fwd)"
     achieved = train_tf_img * args.batch / (ms / 1000.0)   # per GPU, TFLOP/s
     mname = "SD 1.5 UNet (859.5M params)" if sd15 else "SDXL 1.0 UNet (2.567B params)"
+    if args.tiny:
+        mname = f"tiny SDXL-shaped test UNet ({net.num_parameters() / 1e6:.2f}M params; bench-leg test, not a metric)"
     label = "SD1.5 512^2 bf16" if sd15 else "SDXL 1024^2 bf16"
     wl = f"{'SD 1.5' if sd15 else 'SDXL 1.0'} UNet full fine-tune train step {args.res}^2 (latent {args.res // 8}^2), " \
          f"b={args.batch}/GPU, AdamW+bf16 SR, clip 1.0"

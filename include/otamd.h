@@ -308,6 +308,13 @@ int otamd_timestep_embedding(const float* t, int n, int dim, void* out, long lon
 /* replaces: residual add where not fused into a GEMM epilogue */
 int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s);
 
+/* replaces: nothing in the reference (it has no DP): the on-chip footprint of one gradient bucket's RCCL ring
+   all-reduce, emulated on one GPU for the step-slowdown measurement of DESIGN.md §6 (trainer/ddp.py
+   OTAMD_DP_EMULATE): `blocks` workgroups copy `bytes` from src to dst (each wrapping over its size), paced to take
+   at least `ns` nanoseconds */
+int otamd_dp_emulate(const void* src, long long src_bytes, void* dst, long long dst_bytes, long long bytes, int blocks,
+                     long long ns, hipStream_t s);
+
 /* replaces: ModelSetupNoiseMixin._create_noise (modules/modelSetup/mixin/ModelSetupNoiseMixin.py:18-49) */
 int otamd_noise(void* out, int f32, long long n, long long offset, unsigned long long seed, hipStream_t s);
 /* replaces: the same with offset_noise_weight / perturbation_noise_weight > 0 (ModelSetupNoiseMixin.py:31-46):

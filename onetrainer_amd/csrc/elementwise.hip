@@ -372,6 +372,43 @@ OTAMD_API int otamd_add(const void* a, const void* b, void* y, long long n, hipS
   return OTAMD_OK;
 }
 
+// RCCL footprint emulation on one GPU (trainer/ddp.py, OTAMD_DP_EMULATE): a bucket's ring all-reduce
+// over N ranks holds RCCL's channel workgroups on their CUs for its wire time and streams its local HBM bytes.
+// `gridDim.x` workgroups (the channels) copy n16 16-byte vectors, src wrapping over src_n16 and dst over dst_n16,
+// paced by the 100 MHz real-time counter so that workgroup b finishes its share no earlier than `ticks` after
+// it started.  Vector stores only.
+__global__ void __launch_bounds__(256) dp_emulate_kernel(const uint4* __restrict__ src, long long src_n16,
+                                                         uint4* __restrict__ dst, long long dst_n16, long long n16,
+                                                         long long ticks) {
+  const long long per = (n16 + gridDim.x - 1) / gridDim.x;
+  const long long b0 = (long long)blockIdx.x * per, b1 = min(n16, b0 + per);
+  if (b0 >= b1) return;
+  constexpr long long CH = 256 * 8;   // vectors per paced step (32 KiB)
+  const long long nsteps = (b1 - b0 + CH - 1) / CH;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (long long st = 0; st < nsteps; ++st) {
+    const long long base = b0 + st * CH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long long i = base + j * 256 + threadIdx.x;
+      if (i < b1) dst[i % dst_n16] = src[i % src_n16];
+    }
+    const unsigned long long due = t0 + (unsigned long long)((st + 1) * ticks / nsteps);
+    while (__builtin_amdgcn_s_memrealtime() < due) __builtin_amdgcn_s_sleep(4);
+  }
+}
+OTAMD_API int otamd_dp_emulate(const void* src, long long src_bytes, void* dst, long long dst_bytes, long long bytes,
+                               int blocks, long long ns, hipStream_t s) {
+  if (!src || !dst || src_bytes < 16 || dst_bytes < 16 || bytes < 0 || blocks <= 0 || blocks > 4096 || ns < 0 ||
+      !al16(src) || !al16(dst))
+    return OTAMD_EINVAL;
+  if (bytes < 16) return OTAMD_OK;
+  dp_emulate_kernel<<<blocks, 256, 0, s>>>((const uint4*)src, src_bytes / 16, (uint4*)dst, dst_bytes / 16, bytes / 16,
+                                           ns / 10);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
 // Image batch -> VAE encoder input: mgds RescaleImageChannels (0..1 -> -1..1, i.e. x * mul + add;
 // StableDiffusionXLBaseDataLoader.py:66) fused with the NCHW fp32 -> NHWC bf16 relayout, channels
 // zero-padded to cpad (conv_in reads whole 16-byte chunks).  One thread per output pixel.

@@ -1091,6 +1091,13 @@ def add(a, b, out=None):
     return out
 
 
+def dp_emulate(src, dst, nbytes: int, blocks: int, ns: int):
+    """one bucket's RCCL all-reduce footprint on this GPU (trainer/ddp.py OTAMD_DP_EMULATE): `blocks` workgroups
+    copy nbytes from src to dst (wrapping), paced to last at least ns nanoseconds"""
+    check(lib().otamd_dp_emulate(_p(src), src.numel() * src.element_size(), _p(dst), dst.numel() * dst.element_size(),
+                                 int(nbytes), int(blocks), int(ns), stream_handle()), "otamd_dp_emulate")
+
+
 # ------------------------------------------------------------------------------------------
 # diffusion step kernels
 def noise(shape, seed, offset=0, dtype=BF16, device=None, out=None):

@@ -82,9 +82,15 @@ class GenericTrainer(TimedActionMixin):
         if plan is not None and plan.overrides and self.rank == 0:   # util/dtype_util.py: recorded, not silent
             print(f"dtype policy: {plan.summary()}", flush=True)
         self.parameters = self.model.parameters.parameters()
+        import os
+        emulate = int(os.environ.get("OTAMD_DP_EMULATE", "0") or 0)
         if self.world > 1:
             self.reducer = GradBucketReducer(self.model.train_store, bucket_bytes=cfg.dp_bucket_mb << 20,
                                              reduce_fp32=cfg.dp_reduce_fp32)
+        elif emulate > 1 and self.device.type == "cuda":   # RCCL's on-chip footprint at world N, on one GPU (ddp.py)
+            self.reducer = GradBucketReducer(self.model.train_store, bucket_bytes=cfg.dp_bucket_mb << 20, emulate=emulate,
+                                             emulate_blocks=int(os.environ.get("OTAMD_DP_EMULATE_CUS", "64")),
+                                             emulate_gbs=float(os.environ.get("OTAMD_DP_EMULATE_GBS", "400")))
         approx = self.data_loader.get_data_set().approximate_length() if self.data_loader is not None else 1
         self.lr_scheduler = create_lr_scheduler(self.model.optimizer, cfg.learning_rate_scheduler,
                                                 cfg.learning_rate_warmup_steps, cfg.learning_rate_cycles,
@@ -104,7 +110,8 @@ class GenericTrainer(TimedActionMixin):
         from ..module import streams as S
         from ..util.optimizer.adamw_fused import FusedAdamW, OverlappedGradNorm
         opt = getattr(self.model, "optimizer", None)
-        if (isinstance(opt, FusedAdamW) and self.world == 1 and self.graphs is None and self.config.clip_grad_norm
+        if (isinstance(opt, FusedAdamW) and self.world == 1 and self.reducer is None and self.graphs is None
+                and self.config.clip_grad_norm
                 and opt.store.grad.is_cuda and S.enabled() and os.environ.get("OTAMD_NORM_OVERLAP", "1") != "0"
                 and opt.norm_overlap is None):
             opt.norm_overlap = OverlappedGradNorm(opt)

@@ -17,6 +17,12 @@ Gradient accumulation: the reducer is armed only for the backward of an update s
 (`arm(update)` before every backward).  Earlier micro-steps accumulate locally into the grad
 store; the last micro-step's backward launches each bucket once, over the accumulated sum.
 
+Emulation (emulate=N, OTAMD_DP_EMULATE=N in GenericTrainer at world size 1): each bucket's all-reduce is replaced
+by its on-chip footprint on this GPU -- a kernel on the issue stream, at the bucket's ready point, holding
+`emulate_blocks` workgroups (RCCL's channels) for the ring's wire time 2 (N-1)/N S / busbw and moving as many
+bytes through HBM (kernels.dp_emulate) -- so the slowdown RCCL's kernels cause the two compute streams is measured
+on one GPU.  Gradients are left as they are.
+
 Reduction dtype: bf16 in place (default: 2 B/param on the wire, the reference's grad dtype) or,
 with `reduce_fp32=True`, through an fp32 staging copy (4 B/param; one rounding to bf16 after the
 sum instead of one per ring hop).  tests/test_dp_gpu.py characterises both against a world-1
@@ -30,8 +36,21 @@ import torch.distributed as dist
 from ..module import streams as S
 
 
+class _EmulatedWork:
+    """the async-work handle of an emulated bucket: wait() orders the current stream after the issue stream"""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def wait(self):
+        torch.cuda.current_stream().wait_stream(self.stream)
+
+
 class GradBucketReducer:
-    def __init__(self, store, group=None, bucket_bytes: int = 256 << 20, reduce_fp32: bool = False):
+    def __init__(self, store, group=None, bucket_bytes: int = 256 << 20, reduce_fp32: bool = False, emulate: int = 0,
+                 emulate_blocks: int = 64, emulate_gbs: float = 400.0):
+        self.emulate, self.emulate_blocks, self.emulate_gbs = emulate, emulate_blocks, emulate_gbs
+        self.scratch = None
         self.store = store
         self.group = group
         self.reduce_fp32 = reduce_fp32
@@ -86,6 +105,15 @@ class GradBucketReducer:
             self.works.append((self._reduce(g, b, e), bi))
 
     def _reduce(self, g, b, e):
+        if self.emulate > 1:
+            from .. import kernels as K
+            n = self.emulate
+            wire = 2.0 * (n - 1) / n * g.numel() * g.element_size()
+            if self.scratch is None:
+                self.scratch = torch.empty(max(be - bb for bb, be, _ in self.buckets) * g.element_size(),
+                                           dtype=torch.uint8, device=g.device)
+            K.dp_emulate(g, self.scratch, int(wire) // 16 * 16, self.emulate_blocks, int(wire / self.emulate_gbs))
+            return _EmulatedWork(torch.cuda.current_stream())
         if not self.reduce_fp32:
             return dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if self.staging is None:
