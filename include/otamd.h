@@ -308,6 +308,12 @@ int otamd_timestep_embedding(const float* t, int n, int dim, void* out, long lon
 /* replaces: residual add where not fused into a GEMM epilogue */
 int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s);
 
+/* replaces: nothing (engine control): the K-loop schedule of the v2 GEMM tiles, 0 = whole 64-deep K-tile DMA per
+   stage (gemm2_kernel.h), 1 = half-K DMA units with two units in flight across every barrier (gemm2h_kernel.h),
+   2 = half-K units for the MN-mode-A (weight-gradient) GEMMs only; any other value only queries.  Returns the
+   previous schedule.  Default: OTAMD_GEMM_HK, else 0. */
+int otamd_gemm_set_schedule(int hk);
+
 /* replaces: nothing in the reference (it has no DP): the on-chip footprint of one gradient bucket's RCCL ring
    all-reduce, emulated on one GPU for the step-slowdown measurement of DESIGN.md §6 (trainer/ddp.py
    OTAMD_DP_EMULATE): `blocks` workgroups copy `bytes` from src to dst (each wrapping over its size), paced to take

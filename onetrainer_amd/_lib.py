@@ -133,6 +133,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
     "otamd_add": [VP, VP, VP, LL, VP],
     "otamd_dp_emulate": [VP, LL, VP, LL, LL, I, LL, VP],
+    "otamd_gemm_set_schedule": [I],
     "otamd_image_to_nhwc": [VP, I, I, I, I, F, F, VP, I, VP],
     # flux.hip
     "otamd_adaln_fwd": [VP, LL, VP, LL, I, I, F, VP, LL, I, I, I, VP, VP, VP],
