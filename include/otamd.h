@@ -60,6 +60,7 @@ typedef struct GemmArgs {
      GEMM slabs (splits * M floats) and the split-K reduce folds them */
   void* colsum; int colsum_f32; int colsum_acc;
   float* colsum_slab;
+  int* tile_sem;   /* launcher-internal (the in-launch split-K combine's ticket counters): callers leave it 0 */
 } GemmArgs;
 
 typedef struct AttnArgs {
@@ -307,6 +308,26 @@ int otamd_timestep_embedding(const float* t, int n, int dim, void* out, long lon
 
 /* replaces: residual add where not fused into a GEMM epilogue */
 int otamd_add(const void* a, const void* b, void* y, long long n, hipStream_t s);
+
+/* replaces: nothing (engine control): deferred split-K reduces.  Between begin and end, the split-K GEMMs launched on
+   `stream` without bias / row-vector / residual operands whose output (and fused column sums) lie inside
+   [out, out + out_bytes) -- the flat weight-gradient buffer, which only GEMMs on this stream write and nothing reads
+   before a flush -- put their fp32 slabs into `arena` (caller-owned, 256-byte aligned, >= 1 MiB, alive until end)
+   and their reduces are launched together, up to 40 per grouped launch, at flush / end, when the arena or the batch
+   is full, or before a GEMM on the stream reads or writes a pending output.  Each output is summed in split order
+   as by the immediate reduce: bit-identical. */
+int otamd_gemm_defer_begin(hipStream_t stream, void* arena, long long bytes, const void* out, long long out_bytes);
+int otamd_gemm_defer_flush(hipStream_t stream);
+int otamd_gemm_defer_end(hipStream_t stream);
+int otamd_gemm_defer_pending(hipStream_t stream);
+int otamd_gemm_defer_stats(long long* out);
+
+/* replaces: nothing (engine control): the in-launch split-K combine.  A split-K GEMM on the v2 tiles without fused
+   column sums whose per-tile slab traffic (splits * tile bytes in fp32) is at most this many bytes sums its slabs
+   in the workgroup that finishes a tile last (ticket counter, agent-scope release / acquire), bit-identical to
+   the reduce launch it replaces.  Default OTAMD_GEMM_FIXUP_KB (0: always a reduce launch; measured slower in the step), -1 = back to
+   the default.  Returns the previous limit. */
+long long otamd_gemm_set_fixup_limit(long long bytes);   /* out[0] deferred GEMMs, out[1] grouped launches, since load */
 
 /* replaces: nothing (engine control): the K-loop schedule of the v2 GEMM tiles, 0 = whole 64-deep K-tile DMA per
    stage (gemm2_kernel.h), 1 = half-K DMA units with two units in flight across every barrier (gemm2h_kernel.h),

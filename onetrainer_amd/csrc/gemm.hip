@@ -22,7 +22,9 @@
 
 #include <stdlib.h>
 
+#include <atomic>
 #include <mutex>
+#include <unordered_map>
 #include <string.h>
 
 #define BM 128
@@ -304,6 +306,236 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs args, int s
   }
 }
 
+OTAMD_API long long otamd_gemm_ws_bytes(const GemmArgs* in, int splits);
+
+// ---- deferred split-K reduces (otamd_gemm_defer_*) -------------------------------------------------------------------
+// A stream in defer mode puts the fp32 split-K slabs of its eligible GEMMs (no bias / row vector / residual operand,
+// not batched) into a caller-owned arena instead of the workspace and records their reduces; one grouped launch
+// (splitk_reduce_grouped_kernel) later sums up to kMaxDefer of them, each in split order as splitk_reduce_kernel
+// does, so the outputs are bit-identical.  For the weight-gradient stream, where the LoRA adapter gradients (rank
+// 16-32 wide, K = tokens: split-K is inherent) issued ~2,300 reduce launches per SDXL LoRA step.
+struct SplitkDesc {
+  float* slab; void* C; long long ldc;
+  int M, N, splits, flags;   // flags: 1 C fp32, 2 accumulate into C, 4 colsum fp32, 8 accumulate into colsum
+  float alpha; unsigned block0;
+  void* colsum; float* colsum_slab;
+};
+constexpr int kMaxDefer = 40;
+struct SplitkBatch { int n; unsigned blocks; SplitkDesc d[kMaxDefer]; };
+
+__global__ void __launch_bounds__(256) splitk_reduce_grouped_kernel(SplitkBatch bt) {
+  int i = 0;
+  while (i + 1 < bt.n && blockIdx.x >= bt.d[i + 1].block0) ++i;
+  const SplitkDesc& d = bt.d[i];
+  const unsigned nb = (i + 1 < bt.n ? bt.d[i + 1].block0 : bt.blocks) - d.block0;
+  const unsigned lb = blockIdx.x - d.block0;
+  GemmArgs a = {};
+  a.slab = d.slab; a.C = d.C; a.ldc = d.ldc; a.M = d.M; a.N = d.N; a.alpha = d.alpha;
+  a.c_f32 = d.flags & 1; a.accumulate = (d.flags >> 1) & 1;
+  const unsigned NV = (unsigned)d.N / 4;
+  const unsigned total = (unsigned)d.M * NV;
+  for (unsigned e = lb * 256u + threadIdx.x; e < total; e += nb * 256u) {
+    const unsigned m = e / NV, n = (e - m * NV) * 4;
+    splitk_combine<4>(a, m, n, d.splits);
+  }
+  if (d.colsum) {
+    for (unsigned m = lb * 256u + threadIdx.x; m < (unsigned)d.M; m += nb * 256u) {
+      float t = d.colsum_slab[m];
+      for (int z = 1; z < d.splits; ++z) t += d.colsum_slab[(long long)z * d.M + m];
+      if (d.flags & 4) {
+        float* p = reinterpret_cast<float*>(d.colsum) + m;
+        *p = (d.flags & 8) ? *p + t : t;
+      } else {
+        bf16_t* p = reinterpret_cast<bf16_t*>(d.colsum) + m;
+        *p = f2bf((d.flags & 8) ? bf2f(*p) + t : t);
+      }
+    }
+  }
+}
+
+struct DeferState {
+  char* arena = nullptr;
+  long long bytes = 0, used = 0;
+  uintptr_t out_lo = 0, out_hi = 0;   // only outputs inside this range are deferred
+  SplitkBatch batch{};
+  uintptr_t lo[kMaxDefer], hi[kMaxDefer];   // byte ranges each pending reduce writes (C, and the colsum)
+  uintptr_t clo[kMaxDefer], chi[kMaxDefer];
+};
+static std::mutex g_defer_mu;
+static std::unordered_map<hipStream_t, DeferState> g_defer;
+static long long g_defer_gemms = 0, g_defer_launches = 0;   // otamd_gemm_defer_stats
+
+static int defer_flush_locked(DeferState& st, hipStream_t stream) {
+  if (st.batch.n > 0) {
+    splitk_reduce_grouped_kernel<<<st.batch.blocks, 256, 0, stream>>>(st.batch);
+    g_defer_gemms += st.batch.n;
+    ++g_defer_launches;
+    st.batch.n = 0;
+    st.batch.blocks = 0;
+    OTAMD_CHECK_LAUNCH();
+  }
+  st.used = 0;
+  return OTAMD_OK;
+}
+
+static void c_range(const GemmArgs& a, uintptr_t& lo, uintptr_t& hi) {
+  const int es = a.c_f32 ? 4 : 2;
+  lo = (uintptr_t)a.C;
+  hi = lo + ((long long)(a.M - 1) * a.ldc + a.N) * es;
+}
+
+// a GEMM on a deferring stream: a pending reduce whose output this GEMM reads or writes is flushed first
+static int defer_guard(const GemmArgs& a, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  auto it = g_defer.find(stream);
+  if (it == g_defer.end() || it->second.batch.n == 0) return OTAMD_OK;
+  DeferState& st = it->second;
+  uintptr_t lo, hi;
+  c_range(a, lo, hi);
+  const uintptr_t cl = (uintptr_t)a.colsum, ch = cl + (a.colsum ? (uintptr_t)a.M * (a.colsum_f32 ? 4 : 2) : 0);
+  const uintptr_t in[3][2] = {{(uintptr_t)a.A, (uintptr_t)a.A + 1}, {(uintptr_t)a.B, (uintptr_t)a.B + 1}, {lo, hi}};
+  for (int i = 0; i < st.batch.n; ++i) {
+    bool hit = (lo < st.hi[i] && st.lo[i] < hi) || (a.colsum && cl < st.chi[i] && st.clo[i] < ch) ||
+               (a.colsum && cl < st.hi[i] && st.lo[i] < ch);
+    for (int j = 0; j < 2 && !hit; ++j)   // an operand that starts inside a pending output
+      hit = (in[j][0] < st.hi[i] && st.lo[i] < in[j][1]) || (in[j][0] < st.chi[i] && st.clo[i] < in[j][1]);
+    if (hit) return defer_flush_locked(st, stream);
+  }
+  return OTAMD_OK;
+}
+
+// slab memory for a deferrable split-K GEMM on a deferring stream (nullptr: not deferring / not eligible)
+static float* defer_slab(const GemmArgs& a, int splits, hipStream_t stream) {
+  if (a.bias || a.rowvec || a.residual || a.batch > 1) return nullptr;
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  auto it = g_defer.find(stream);
+  if (it == g_defer.end()) return nullptr;
+  DeferState& st = it->second;
+  uintptr_t lo, hi;
+  c_range(a, lo, hi);
+  if (lo < st.out_lo || hi > st.out_hi) return nullptr;
+  if (a.colsum) {
+    const uintptr_t cl = (uintptr_t)a.colsum, ch = cl + (uintptr_t)a.M * (a.colsum_f32 ? 4 : 2);
+    if (cl < st.out_lo || ch > st.out_hi) return nullptr;
+  }
+  const long long need = (otamd_gemm_ws_bytes(&a, splits) + 255) / 256 * 256;
+  if (need > st.bytes) return nullptr;
+  if (st.batch.n == kMaxDefer || st.used + need > st.bytes) defer_flush_locked(st, stream);
+  float* p = reinterpret_cast<float*>(st.arena + st.used);
+  st.used += need;
+  return p;
+}
+
+static void defer_record(const GemmArgs& a, int splits, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  DeferState& st = g_defer[stream];
+  SplitkDesc& d = st.batch.d[st.batch.n];
+  d.slab = a.slab; d.C = a.C; d.ldc = a.ldc; d.M = a.M; d.N = a.N; d.splits = splits; d.alpha = a.alpha;
+  d.flags = (a.c_f32 ? 1 : 0) | (a.accumulate ? 2 : 0) | (a.colsum_f32 ? 4 : 0) | (a.colsum_acc ? 8 : 0);
+  d.colsum = a.colsum; d.colsum_slab = a.colsum_slab;
+  d.block0 = st.batch.blocks;
+  const long long nv = (long long)a.M * a.N / 4;
+  st.batch.blocks += (unsigned)std::min<long long>((std::max<long long>(nv, a.M) + 255) / 256, 2048);
+  c_range(a, st.lo[st.batch.n], st.hi[st.batch.n]);
+  st.clo[st.batch.n] = (uintptr_t)a.colsum;
+  st.chi[st.batch.n] = (uintptr_t)a.colsum + (a.colsum ? (uintptr_t)a.M * (a.colsum_f32 ? 4 : 2) : 0);
+  ++st.batch.n;
+}
+
+// start deferring this stream's split-K reduces of outputs inside [out, out + out_bytes) into `arena` (>= 1 MiB,
+// 256-byte aligned; the caller keeps it alive until otamd_gemm_defer_end); pending reduces of an earlier begin are
+// flushed first
+OTAMD_API int otamd_gemm_defer_begin(hipStream_t stream, void* arena, long long bytes, const void* out,
+                                     long long out_bytes) {
+  if (!arena || ((uintptr_t)arena & 255) || bytes < (1 << 20) || !out || out_bytes <= 0) return OTAMD_EINVAL;
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  DeferState& st = g_defer[stream];
+  defer_flush_locked(st, stream);
+  st.arena = (char*)arena;
+  st.bytes = bytes;
+  st.used = 0;
+  st.out_lo = (uintptr_t)out;
+  st.out_hi = (uintptr_t)out + (uintptr_t)out_bytes;
+  return OTAMD_OK;
+}
+// launch the grouped reduce of every pending GEMM on this stream (stream-ordered); a no-op when none is pending
+OTAMD_API int otamd_gemm_defer_flush(hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  auto it = g_defer.find(stream);
+  return it == g_defer.end() ? OTAMD_OK : defer_flush_locked(it->second, stream);
+}
+// flush and leave defer mode
+OTAMD_API int otamd_gemm_defer_end(hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  auto it = g_defer.find(stream);
+  if (it == g_defer.end()) return OTAMD_OK;
+  const int rc = defer_flush_locked(it->second, stream);
+  g_defer.erase(it);
+  return rc;
+}
+// totals since load: out[0] = GEMMs whose reduce was deferred, out[1] = grouped reduce launches
+OTAMD_API int otamd_gemm_defer_stats(long long* out) {
+  if (!out) return OTAMD_EINVAL;
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  out[0] = g_defer_gemms;
+  out[1] = g_defer_launches;
+  return OTAMD_OK;
+}
+// reduces pending on this stream
+OTAMD_API int otamd_gemm_defer_pending(hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  auto it = g_defer.find(stream);
+  return it == g_defer.end() ? 0 : it->second.batch.n;
+}
+
+// ---- in-launch split-K combine (splitk_fixup, gemm.h) -------------------------------------------------------------
+// Per-stream ticket counters, zeroed once when allocated and left zero by every launch (the last arriver resets its
+// tile's word).  A split-K GEMM of the v2 tiles without fused column sums whose per-tile slab traffic
+// (splits * BM * BN * 4 bytes) is at most OTAMD_GEMM_FIXUP_KB (default 0 = off: measured slower) combines in-launch instead of
+// launching splitk_reduce_kernel.  Never allocated under stream capture (that launch keeps the reduce launch).
+constexpr int kSemTiles = 1 << 16;
+static std::mutex g_sem_mu;
+static std::unordered_map<hipStream_t, int*> g_sem;
+
+static long long fixup_limit() {
+  static const long long kb = [] {
+    const char* e = getenv("OTAMD_GEMM_FIXUP_KB");
+    return e ? atoll(e) : 0LL;
+  }();
+  return kb << 10;
+}
+static std::atomic<long long> g_fixup_override{-1};
+// A/B: force the in-launch combine's per-tile byte limit (bytes; -1 = OTAMD_GEMM_FIXUP_KB); returns the previous
+OTAMD_API long long otamd_gemm_set_fixup_limit(long long bytes) {
+  const long long prev = g_fixup_override.exchange(bytes);
+  return prev < 0 ? fixup_limit() : prev;
+}
+
+static int* tile_sems(hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_sem_mu);
+  auto it = g_sem.find(stream);
+  if (it != g_sem.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  int* p = nullptr;
+  if (hipMalloc(&p, kSemTiles * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, kSemTiles * sizeof(int)) != hipSuccess) { (void)hipFree(p); return nullptr; }
+  g_sem[stream] = p;
+  return p;
+}
+
+static int* fixup_sems(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
+  static const int geo[11][2] = {{256, 256}, {256, 128}, {128, 256}, {256, 256}, {128, 128}, {128, 64},
+                                 {64, 128},  {128, 160}, {256, 160}, {128, 64},  {64, 128}};
+  if (splits <= 1 || tile < 0 || tile > 10 || a.colsum || a.batch > 1) return nullptr;
+  const long long ov = g_fixup_override.load(std::memory_order_relaxed);
+  const long long lim = ov >= 0 ? ov : fixup_limit();
+  const int bm = geo[tile][0], bn = geo[tile][1];
+  if ((long long)splits * bm * bn * 4 > lim) return nullptr;
+  if ((long long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) > kSemTiles) return nullptr;
+  return tile_sems(stream);
+}
+
 typedef void (*gemm_fn)(GemmArgs);
 
 static gemm_fn pick(int am, int bm) {
@@ -462,6 +694,7 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
                      hipStream_t stream) {
   if (!in) return OTAMD_EINVAL;
   GemmArgs a = *in;
+  a.tile_sem = nullptr;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
   const bool v2_only = a.bmode == OPM_CONV_WT || a.A2 != nullptr;
   if (a.A2) {   // second K segment (LoRA fusion): forms and alignment the v2 kernels support
@@ -495,11 +728,19 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   long long kps = ((long long)(a.K + splits - 1) / splits + BK - 1) / BK * BK;
   splits = (int)((a.K + kps - 1) / kps);
   a.k_per_split = (int)kps;
+  if (const int rc = defer_guard(a, stream)) return rc;
+  bool deferred = false;
   if (splits > 1) {
     // the split-K reduce indexes M * N in 32 bits: refuse before anything is launched
     if ((long long)a.M * a.N >= (1LL << 32)) return OTAMD_EINVAL;
-    if (!workspace || ws_bytes < otamd_gemm_ws_bytes(&a, splits) || !aligned16(workspace)) return OTAMD_EINVAL;
-    a.slab = (float*)workspace;
+    float* ds = defer_slab(a, splits, stream);
+    if (ds) {
+      deferred = true;
+      a.slab = ds;
+    } else {
+      if (!workspace || ws_bytes < otamd_gemm_ws_bytes(&a, splits) || !aligned16(workspace)) return OTAMD_EINVAL;
+      a.slab = (float*)workspace;
+    }
     a.colsum_slab = a.colsum ? a.slab + (long long)splits * a.M * a.N : nullptr;
   } else {
     a.slab = nullptr;
@@ -510,16 +751,21 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   if (a.colsum && (tile < 0 || tile == 3)) tile = 0;   // the fused column sums live in the 8-wave v2 kernels
   if (v2_only && tile < 0) return OTAMD_EUNSUPPORTED;
   int rc = OTAMD_EUNSUPPORTED;
+  if (!deferred) a.tile_sem = fixup_sems(a, tile, splits, stream);
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
+  const bool combined = rc == OTAMD_OK && a.tile_sem != nullptr;   // the v2 kernel combined its splits in-launch
   if (rc != OTAMD_OK) {
+    a.tile_sem = nullptr;
     if (!fn || a.A2 || a.colsum) return rc;   // v1 has no conv-weight B, no second K segment, no column sums
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid(tiles, a.batch > 1 ? a.batch : 1, splits);
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);
     OTAMD_CHECK_LAUNCH();
   }
-  if (splits > 1) {
+  if (deferred) {
+    defer_record(a, splits, stream);
+  } else if (splits > 1 && !combined) {
     // 8-wide needs 16-byte aligned rows of C (bf16: ldc % 8, fp32 handled element-wise)
     const bool v8 = (a.N % 8) == 0 && (a.ldc % 8) == 0 && ((uintptr_t)a.C & 15) == 0;
     const long long nv = (long long)a.M * a.N / (v8 ? 8 : 4);

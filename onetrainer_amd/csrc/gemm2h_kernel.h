@@ -433,6 +433,7 @@ gemm2h_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes, unsigned, unsig
         }
       }
     }
+    if (use_slab && args.tile_sem) splitk_fixup<BM, BN>(args, m0, n0, reinterpret_cast<int*>(smem));
     return;
   }
 #pragma unroll

@@ -57,6 +57,40 @@ def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     return ws
 
 
+_DEFER_ARENAS: dict = {}   # raw stream -> persistent arena of its deferred split-K slabs
+
+
+def defer_reduces_begin(stream, grads: torch.Tensor, nbytes: int = 256 << 20) -> None:
+    """defer the split-K reduces of the weight-gradient GEMMs launched on `stream` (a torch Stream) that write into
+    `grads` (the flat gradient buffer) and launch them grouped (otamd_gemm_defer_begin: bit-identical, one launch
+    per up to 40 GEMMs)"""
+    key = stream.cuda_stream
+    ar = _DEFER_ARENAS.get(key)
+    if ar is None or ar.numel() < nbytes:
+        ar = _DEFER_ARENAS[key] = torch.empty(nbytes, dtype=torch.uint8, device=stream.device)
+    check(lib().otamd_gemm_defer_begin(C.c_void_p(key), _p(ar), ar.numel(), _p(grads),
+                                       grads.numel() * grads.element_size()), "otamd_gemm_defer_begin")
+
+
+def defer_reduces_flush(stream) -> None:
+    check(lib().otamd_gemm_defer_flush(C.c_void_p(stream.cuda_stream)), "otamd_gemm_defer_flush")
+
+
+def defer_reduces_end(stream) -> None:
+    check(lib().otamd_gemm_defer_end(C.c_void_p(stream.cuda_stream)), "otamd_gemm_defer_end")
+
+
+def defer_reduces_stats() -> tuple:
+    """(GEMMs whose split-K reduce went out deferred, grouped reduce launches) since the library loaded"""
+    out = (C.c_longlong * 2)()
+    check(lib().otamd_gemm_defer_stats(C.cast(out, C.c_void_p)), "otamd_gemm_defer_stats")
+    return int(out[0]), int(out[1])
+
+
+def defer_reduces_pending(stream) -> int:
+    return int(lib().otamd_gemm_defer_pending(C.c_void_p(stream.cuda_stream)))
+
+
 _gemm_forced_splits = 0   # tools/gemm_splits.py probe: forces the split count of planned GEMMs
 
 # ---- GEMM plan autotuner --------------------------------------------------------------------

@@ -138,12 +138,16 @@ class FlatParamStore:
     def begin_backward(self):
         self.wait_params()   # backward overwrites the gradients the optimizer chunks read
         self._written.clear()
+        if self.device.type == "cuda":
+            from .streams import defer_begin
+            defer_begin(self.grad if self.trainable else None)   # the gradient GEMMs' split-K reduces go out grouped
 
     def finish_backward(self):
         """join the weight-gradient stream, then zero the grads of parameters that received none
         this micro-step (overwrite semantics)."""
         if self.device.type == "cuda":
-            from .streams import join
+            from .streams import defer_end, join
+            defer_end()      # the pending grouped split-K reduces, before anything reads the gradients
             join()
         if self.trainable and not self.accumulating:
             for n in self.order:

@@ -100,6 +100,33 @@ def note_side(tensors, depth: int = 1):
             h.side_read(tensors, label)
 
 
+_DEFER = os.environ.get("OTAMD_DEFER_REDUCE", "1") != "0"
+
+
+def defer_begin(grads):
+    """start of a backward: the side stream's split-K reduces into the flat gradient buffer `grads` are deferred and
+    launched grouped (kernels.defer_reduces_begin; OTAMD_DEFER_REDUCE=0 launches each with its GEMM)"""
+    side = side_stream()
+    if side is not None and _DEFER and grads is not None and grads.numel():
+        from .. import kernels as K
+        K.defer_reduces_begin(side, grads)
+
+
+def defer_flush():
+    """before anything reads weight gradients the side stream produced (norm chunks, DP buckets, the join)"""
+    side = side_stream()
+    if side is not None and _DEFER:
+        from .. import kernels as K
+        K.defer_reduces_flush(side)
+
+
+def defer_end():
+    side = side_stream()
+    if side is not None and _DEFER:
+        from .. import kernels as K
+        K.defer_reduces_end(side)
+
+
 def join():
     """make the current stream wait for all weight-gradient work queued so far."""
     side = side_stream()

@@ -100,6 +100,7 @@ class GradBucketReducer:
         s.wait_stream(torch.cuda.current_stream())
         side = S.side_stream()
         if side is not None:
+            S.defer_flush()   # the deferred split-K reduces of the side stream write into this bucket
             s.wait_stream(side)
         with torch.cuda.stream(s):
             self.works.append((self._reduce(g, b, e), bi))

@@ -288,6 +288,8 @@ class OverlappedGradNorm:
         g = opt.store.grad
         dtype = 0 if g.dtype == torch.bfloat16 else 1
         if side is not None:
+            from ...module import streams as S
+            S.defer_flush()   # the bucket's deferred split-K reduces (module/streams.py) before its norms
             self._ev.record(torch.cuda.current_stream())
             side.wait_event(self._ev)
             with torch.cuda.stream(side):

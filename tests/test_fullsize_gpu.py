@@ -7,8 +7,9 @@ weights, same bf16-rounded inputs, same injected noise / timesteps):
   * SD 1.5 `sd15_config()` (8 heads of 40/80/160, ctx 768) at 512^2 b=1 -- C1's shape;
   * FLUX.1 at full width (D = 3072, 24 x 128 heads, T5 ctx 4096) with 1 double + 1 single block at
     768^2 b=1 (2304 image tokens + 77 text tokens).
+  * the SDXL UNet with C4's rank-32 LoRA on every Linear / Conv2d (oracle/lora.py hooks) at 512^2 b=1.
   Each checks the diffusion loss to rtol 1e-3 (north star), the prediction's element-wise cosine and every
-  parameter gradient's cosine.
+  parameter (adapter) gradient's cosine.
 
 Full-size property steps at the BASELINE workloads (too large for a CPU oracle):
   * C2 SD 1.5 FT 512^2 b=16, C3 SDXL FT 1024^2 b=4 (per-rank batch of the DP-8 config),
@@ -94,6 +95,62 @@ def test_full_unet_matches_oracle(dev, name, res):
     assert cos[0][0] > 0.98, cos[:4]
     assert sum(c for c, _ in cos) / len(cos) > 0.999
     del m, om
+    _free()
+
+
+def test_full_width_sdxl_lora_r32_matches_oracle(dev):
+    """C4's adapter set at full width: the SDXL UNet (frozen bf16 base) with rank-32 LoRA on every Linear / Conv2d
+    (module/lora.py: fused down / block-diagonal up, second-K-segment GEMMs, deferred split-K weight-gradient reduces)
+    against the oracle UNet with the reference LoRA hooks (oracle/lora.py; LoRAModule.py:283-323) at 512^2 b=1:
+    diffusion loss to rtol 1e-3, the prediction's cosine, and every adapter gradient's cosine."""
+    from onetrainer_amd.module.lora import LoRAUNetWrapper
+    from oracle.lora import OracleLoRA
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    cfg = U.sdxl_config()
+    m = U.UNet2DConditionModel(cfg, dev, seed=1, trainable=False)
+    om = _oracle_unet(cfg, m)
+    om.requires_grad_(False)
+    rank, alpha = 32, 16.0
+    lw = LoRAUNetWrapper(m, rank=rank, alpha=alpha, seed=0)
+    m.lora = lw
+    ol = OracleLoRA(om, rank, alpha)
+    g = torch.Generator().manual_seed(3)
+    # random up weights too (the reference initialises them to zero): every adapter then shapes the output and
+    # receives a gradient through both of its factors
+    sd = {k: (torch.randn(v.shape, generator=g) * (0.02 if "lora_up" in k else 0.05) if not k.endswith(".alpha") else v)
+          for k, v in lw.state_dict().items()}
+    lw.load_state_dict(sd)
+    ol.load_state_dict({k: v for k, v in lw.state_dict().items() if not k.endswith(".alpha")})
+    B, h, res = 1, 64, 512
+    x0 = torch.randn(B, 4, h, h, generator=g)
+    eps = torch.randn(B, 4, h, h, generator=g)
+    t = torch.tensor([311], dtype=torch.int32)
+    ehs = torch.randn(B, 77, cfg.cross_attention_dim, generator=g).bfloat16()
+    te = torch.randn(B, 1280, generator=g).bfloat16()
+    tid = torch.tensor([[float(res), float(res), 0., 0., float(res), float(res)]])
+    xt = OD.add_noise_ddpm(x0, eps, t.long(), OD.scaled_linear_betas()).bfloat16()
+    xin = torch.zeros(B, h, h, 8, dtype=torch.bfloat16)
+    xin[..., :4] = xt.permute(0, 2, 3, 1)
+    out = m(xin.to(dev), t.to(dev), ehs.to(dev), te.to(dev), tid.to(dev))
+    loss, coef, _ = K.mse_loss(out, eps.permute(0, 2, 3, 1).contiguous().to(dev))
+    ref = om(xt.float(), t.long(), ehs.float(), te.float(), tid)
+    ref_loss = OD.diffusion_losses(ref, eps, torch.ones(B)).mean()
+    pcos = _cos(out[..., :4].float().cpu().permute(0, 3, 1, 2), ref.detach())
+    print(f"sdxl lora r32 512^2 loss hip {loss.item():.6f} oracle {ref_loss.item():.6f} prediction cosine {pcos:.6f}")
+    assert abs(loss.item() - ref_loss.item()) <= 1e-3 * abs(ref_loss.item())
+    assert pcos > 0.999, pcos
+    lw.store.begin_backward()
+    out.backward(K.mse_grad(out, eps.permute(0, 2, 3, 1).contiguous().to(dev), coef))
+    lw.store.finish_backward()
+    ref_loss.backward()
+    gs = lw.state_dict(grads=True)
+    cos = sorted((_cos(gs[k].float().cpu().reshape(p.shape), p.grad), k) for k, p in ol.params.items())
+    print(f"{len(cos)} adapter tensors; worst grad cosines:", cos[:4])
+    assert len(cos) > 1500
+    assert cos[0][0] > 0.98, cos[:4]
+    assert sum(c for c, _ in cos) / len(cos) > 0.999
+    assert m.store.grad is None
+    del m, om, lw, ol
     _free()
 
 
