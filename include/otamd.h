@@ -235,6 +235,14 @@ int otamd_layernorm_bwd_res(const void* x, long long ldx, const void* dy, long l
     long long ldres, void* dx, long long lddx, int rows, int C, const void* gamma, const float* mean,
     const float* rstd, hipStream_t stream);
 
+/* replaces: the same backward (+ the residual gradient dres, nullable; or + dx when accumulate) AND
+   dgamma / dbeta in one pass over x and dy (otamd_layernorm_bwd_res + otamd_layernorm_param_grad read both twice);
+   part: float scratch >= 1024 * 2 * C.  OTAMD_EUNSUPPORTED (nothing launched) for widths without a row-group form. */
+int otamd_layernorm_bwd_fused(const void* x, long long ldx, const void* dy, long long lddy, const void* dres,
+                              long long ldres, void* dx, long long lddx, int rows, int C, const void* gamma,
+                              const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32,
+                              int param_acc, float* part, int accumulate, hipStream_t stream);
+
 /* replaces: the LayerNorm weight / bias gradient half of the same autograd node (dgamma = sum dy xhat,
    dbeta = sum dy), issued separately so it can run on the weight-gradient side stream */
 int otamd_layernorm_param_grad(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,

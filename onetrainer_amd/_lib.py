@@ -103,6 +103,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_layernorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],
     "otamd_layernorm_param_grad": [VP, LL, VP, LL, I, I, VP, VP, VP, VP, I, I, VP, VP],
     "otamd_layernorm_bwd_res": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP],
+    "otamd_layernorm_bwd_fused": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],
     # attention.hip
     "otamd_attn_args_size": [],
     "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],

@@ -774,6 +774,32 @@ def layernorm_bwd_res(x, dy, dres, gamma, stats):
     return dx
 
 
+def layernorm_bwd_fused(x, dy, gamma, stats, dgamma, dbeta, dres=None, param_acc=False):
+    """dx = LayerNorm-backward(dy) (+ dres) and dgamma / dbeta (= or +=) from one read of x and dy; None when the
+    width has no fused form (the caller then runs layernorm_bwd(_res) + layernorm_param_grad)."""
+    h = _host()
+    if h is not None:
+        return h.layernorm_bwd_fused(x, dy, dres, gamma, stats[0], stats[1], dgamma, dbeta, param_acc, stream_handle())
+    rows, C_, ldx = _rows2d(x)
+    _, _, lddy = _rows2d(dy)
+    _req(dgamma.dtype == dbeta.dtype and dgamma.dtype in (BF16, F32), "layernorm param grads bf16 / f32")
+    ldres = 0
+    if dres is not None:
+        _req(dres.shape == x.shape and dres.dtype == BF16, "layernorm residual grad: bf16, shape of x")
+        _, _, ldres = _rows2d(dres)
+    dx = torch.empty(x.shape, dtype=BF16, device=x.device)
+    _, _, lddx = _rows2d(dx)
+    part = workspace(1024 * 2 * C_ * 4, x.device)
+    mean, rstd = stats
+    rc = lib().otamd_layernorm_bwd_fused(_p(x), ldx, _p(dy), lddy, _p(dres) if dres is not None else None, ldres,
+                                         _p(dx), lddx, rows, C_, _p(gamma), _p(mean), _p(rstd), _p(dgamma), _p(dbeta),
+                                         int(dgamma.dtype == F32), int(param_acc), _p(part), 0, stream_handle())
+    if rc == 3:   # OTAMD_EUNSUPPORTED
+        return None
+    check(rc, "otamd_layernorm_bwd_fused")
+    return dx
+
+
 def layernorm_param_grad(x, dy, stats, dgamma, dbeta, param_acc=False):
     """dgamma += / = sum_rows dy * xhat, dbeta = sum_rows dy (bf16 or f32 destinations)."""
     h = _host()
