@@ -43,6 +43,7 @@ struct AttnArgs {
 };
 
 #define KT 64   // keys per staged tile (fwd / dQ)
+#define RESCALE_T 8.0f   // forward: lazy-max threshold (log2 units)
 #define OFF_INVALID 0x80000000u
 static constexpr float LOG2E = 1.4426950408889634f;
 
@@ -420,10 +421,12 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
       float tmax = S[0];
 #pragma unroll
       for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, S[i]);
-      tmax = fmaxf(tmax, xor32(tmax));
-      const float mc = tmax * c;
-      if (__builtin_amdgcn_ballot_w64(mc > m) != 0) {   // wave-uniform: some row max grew
-        const float mn = fmaxf(m, mc);
+      // lazy max (cdna_hip_programming.md T13): m only moves when a score of this lane's half-row exceeds it by more
+      // than RESCALE_T (log2 units), so P <= 2^RESCALE_T otherwise; any m >= -inf normalises out of O / l and the
+      // LSE (m + log2 l), and O and l always see the same factor.  The full row max (the half-rows' xor32) is needed
+      // only on that wave-uniform branch.
+      if (__builtin_amdgcn_ballot_w64(tmax * c > m + RESCALE_T) != 0) {
+        const float mn = fmaxf(m, fmaxf(tmax, xor32(tmax)) * c);
         const float alpha = __builtin_amdgcn_exp2f(m - mn);
         l *= alpha;
         if constexpr (D == 64) {
@@ -459,8 +462,7 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
         for (int k = 1; k < 8; ++k) rs2 += f2v{S[2 * k], S[2 * k + 1]};
         rs = rs2.x + rs2.y;
       }
-      rs += xor32(rs);
-      l += rs;
+      l += rs;   // this lane's half-row (the halves meet once, after the loop)
       const bf16x8 p0 = pack_acc(S, 0), p1 = pack_acc(S, 1);
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
@@ -470,6 +472,7 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
     }
   };
   stage_loop_last<NS, (D <= 64)>(ntiles, step);
+  l += xor32(l);
   const int q = q0 + r;
   const float inv = 1.f / l;
   bf16_t* Op = a.o + b * a.bso + (long long)min(q, a.Nq - 1) * a.ldo + hh * a.Dv;
