@@ -484,9 +484,9 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
 // dQ: per wave 32 queries, iterate over key tiles (a dual-use K image -- row reads for S, transposed reads for
 // dQ -- and a V image per stage)
 // NS = LDS ring depth, KTD = keys per tile.  Launched as (otamd_attn_bwd):
-//   D = 64:  <64, 3> -- 32-key tiles 3 deep (24 KiB: one dual-use K image and one V image per stage); three
-//            blocks per CU (__launch_bounds__(256, 3), set by the VGPRs), so the SDXL level-2 grid
-//            (8 x 20 heads x 4 = 640 blocks) runs in one round of 768 slots
+//   D = 64:  <64, 3> -- 64-key tiles (two 32-key sub-tiles per barrier) 3 deep (48 KiB: one dual-use K image and
+//            one V image per stage); three blocks per CU (__launch_bounds__(256, 3), set by the VGPRs), so the SDXL
+//            level-2 grid (8 x 20 heads x 4 = 640 blocks) runs in one round of 768 slots
 //   D = 128: <128, 2, 64> -- 64-key tiles 2 deep (64 KiB), two blocks per CU: 1086 us per Flux call
 //            (4 x 2381 x 24 heads) against 1104 us for 32-key tiles 3 deep (round 4, same box)
 template <int D, int NS, int KTD = KT>
