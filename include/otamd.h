@@ -167,6 +167,13 @@ int otamd_adaln_bwd(const void* x, long long ldx, const void* dy, long long lddy
                     int D, const void* mod, long long ldm, int shift_off, int scale_off, int B, const float* mean,
                     const float* rstd, void* dmod, float* part, hipStream_t s);
 
+/* the same + res (the adaLN input's gradient through its residual use, the block's gated add) in the dx pass,
+   instead of autograd's separate add of the two contributions */
+int otamd_adaln_bwd_res(const void* x, long long ldx, const void* dy, long long lddy, const void* res, long long ldres,
+                        void* dx, long long lddx, int rows, int D, const void* mod, long long ldm, int shift_off,
+                        int scale_off, int B, const float* mean, const float* rstd, void* dmod, float* part,
+                        hipStream_t s);
+
 /* scratch floats the adaLN / gated-add backward reductions need */
 long long otamd_mod_part_floats(int T, int D, int B);
 

@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(256) adaln_bwd_dx_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ dx, long long lddx, int rows, int D,
                                                            const bf16_t* __restrict__ mod, long long ldm, int scale_off,
                                                            int B, const float* __restrict__ mean_in,
-                                                           const float* __restrict__ rstd_in) {
+                                                           const float* __restrict__ rstd_in,
+                                                           const bf16_t* __restrict__ res, long long ldres) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -111,6 +112,12 @@ __global__ void __launch_bounds__(256) adaln_bwd_dx_kernel(const bf16_t* __restr
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+      if (res) {   // + the input's gradient through its residual use (the block's gated add)
+        float rv[8];
+        ld8(res + (long long)row * ldres + c8 * 8, rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += rv[j];
+      }
       st8(dx + (long long)row * lddx + c8 * 8, o);
     }
   }
@@ -441,15 +448,18 @@ static int mod_splits(int T, int D, int B) {
 // float scratch the adaLN / gated backward reductions need (pass as `part`)
 OTAMD_API long long otamd_mod_part_floats(int T, int D, int B) { return 2LL * mod_splits(T, D, B) * B * D; }
 
-// rows = T * B; dmod gets bf16(dscale) at scale_off and bf16(dshift) at shift_off (overwrite)
-OTAMD_API int otamd_adaln_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long lddx,
-                              int rows, int D, const void* mod, long long ldm, int shift_off, int scale_off, int B,
-                              const float* mean, const float* rstd, void* dmod, float* part, hipStream_t s) {
+// rows = T * B; dmod gets bf16(dscale) at scale_off and bf16(dshift) at shift_off (overwrite); res (nullable):
+// dx += res in the same pass
+static int adaln_bwd_impl(const void* x, long long ldx, const void* dy, long long lddy, const void* res, long long ldres,
+                          void* dx, long long lddx, int rows, int D, const void* mod, long long ldm, int shift_off,
+                          int scale_off, int B, const float* mean, const float* rstd, void* dmod, float* part,
+                          hipStream_t s) {
   if (!x || !dy || !dx || !mod || !mean || !rstd || rows <= 0 || B <= 0 || rows % B || D % 8 || D > 512 * AD_MAXCH ||
-      ldx % 8 || lddy % 8 || lddx % 8 || ldm % 8 || !a16(x) || !a16(dy) || !a16(dx))
+      ldx % 8 || lddy % 8 || lddx % 8 || ldm % 8 || !a16(x) || !a16(dy) || !a16(dx) || (res && (ldres % 8 || !a16(res))))
     return OTAMD_EINVAL;
   adaln_bwd_dx_kernel<<<(rows + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, (bf16_t*)dx,
-                                                     lddx, rows, D, (const bf16_t*)mod, ldm, scale_off, B, mean, rstd);
+                                                     lddx, rows, D, (const bf16_t*)mod, ldm, scale_off, B, mean, rstd,
+                                                     (const bf16_t*)res, ldres);
   OTAMD_CHECK_LAUNCH();
   if (dmod) {
     if (!part) return OTAMD_EINVAL;
@@ -462,6 +472,21 @@ OTAMD_API int otamd_adaln_bwd(const void* x, long long ldx, const void* dy, long
     OTAMD_CHECK_LAUNCH();
   }
   return OTAMD_OK;
+}
+
+OTAMD_API int otamd_adaln_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long lddx,
+                              int rows, int D, const void* mod, long long ldm, int shift_off, int scale_off, int B,
+                              const float* mean, const float* rstd, void* dmod, float* part, hipStream_t s) {
+  return adaln_bwd_impl(x, ldx, dy, lddy, nullptr, 0, dx, lddx, rows, D, mod, ldm, shift_off, scale_off, B, mean, rstd,
+                        dmod, part, s);
+}
+OTAMD_API int otamd_adaln_bwd_res(const void* x, long long ldx, const void* dy, long long lddy, const void* res,
+                                  long long ldres, void* dx, long long lddx, int rows, int D, const void* mod,
+                                  long long ldm, int shift_off, int scale_off, int B, const float* mean,
+                                  const float* rstd, void* dmod, float* part, hipStream_t s) {
+  if (!res) return OTAMD_EINVAL;
+  return adaln_bwd_impl(x, ldx, dy, lddy, res, ldres, dx, lddx, rows, D, mod, ldm, shift_off, scale_off, B, mean, rstd,
+                        dmod, part, s);
 }
 
 OTAMD_API int otamd_gated_add_fwd(const void* x, long long ldx, const void* y, long long ldy, void* out, long long ldo,

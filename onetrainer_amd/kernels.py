@@ -1295,7 +1295,8 @@ def adaln_fwd(x, mod, shift_off, scale_off, B, eps=1e-6, out=None):
     return out, (mean, rstd)
 
 
-def adaln_bwd(x, dy, mod, shift_off, scale_off, B, stats, dmod=None, dx=None):
+def adaln_bwd(x, dy, mod, shift_off, scale_off, B, stats, dmod=None, dx=None, dres=None):
+    """dx (+ dres: the input's gradient through its residual use, summed in the same pass)"""
     rows, D, ldx = _rows2d(x)
     _, _, lddy = _rows2d(dy)
     _mod_ok(mod, B, shift_off, scale_off)
@@ -1307,6 +1308,13 @@ def adaln_bwd(x, dy, mod, shift_off, scale_off, B, stats, dmod=None, dx=None):
         _req(dmod.shape == mod.shape and dmod.stride() == mod.stride(), "dmod like mod")
         part = _mod_part(rows // B, D, B, x.device)
     mean, rstd = stats
+    if dres is not None:
+        _req(dres.shape == (rows, D) and dres.dtype == BF16, "adaln residual grad: bf16 [rows, D]")
+        _, _, ldres = _rows2d(dres)
+        check(lib().otamd_adaln_bwd_res(_p(x), ldx, _p(dy), lddy, _p(dres), ldres, _p(dx), lddx, rows, D, _p(mod),
+                                        mod.stride(0), shift_off, scale_off, B, _p(mean), _p(rstd), _p(dmod), _p(part),
+                                        stream_handle()), "otamd_adaln_bwd_res")
+        return dx
     check(lib().otamd_adaln_bwd(_p(x), ldx, _p(dy), lddy, _p(dx), lddx, rows, D, _p(mod), mod.stride(0), shift_off,
                                 scale_off, B, _p(mean), _p(rstd), _p(dmod), _p(part), stream_handle()),
           "otamd_adaln_bwd")

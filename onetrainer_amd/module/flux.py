@@ -16,6 +16,7 @@ MI355X layout (not a translation of the diffusers module tree):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -45,6 +46,18 @@ class FluxConfig:
     @property
     def inner_dim(self) -> int:
         return self.num_attention_heads * self.attention_head_dim
+
+
+
+# the blocks' adaLN inputs are also their residuals: AdaLNResFn sums the two gradient contributions inside the adaLN
+# backward (OTAMD_ADALN_RES=0: autograd adds them, the A/B reference)
+_ADALN_RES = os.environ.get("OTAMD_ADALN_RES", "1") != "0"
+
+
+def _adaln_res(hx, emb, st, segs, B):
+    if _ADALN_RES:
+        return O.AdaLNResFn.apply(hx, emb, st, segs, B)
+    return O.AdaLNFn.apply(hx, emb, st, segs, B), hx
 
 
 def flux_dev_config() -> FluxConfig:
@@ -301,7 +314,7 @@ class FluxTransformer2DModel:
             p = f"transformer_blocks.{i}."
             emb, st, o = mod[p + "norm1.linear"]
             embc, stc, oc = mod[p + "norm1_context.linear"]
-            n = O.AdaLNFn.apply(hx, emb, st, [(0, LB, oc, oc + D), (LB, TB, o, o + D)], B)
+            n, hx = _adaln_res(hx, emb, st, [(0, LB, oc, oc + D), (LB, TB, o, o + D)], B)
             wi, bi, si = self._fused_lin([p + "attn.to_q", p + "attn.to_k", p + "attn.to_v"], D)
             wc, bc, sc = self._fused_lin([p + "attn.add_q_proj", p + "attn.add_k_proj", p + "attn.add_v_proj"], D)
             qkv = O.rows_linear(n, [(0, LB, wc, bc, sc), (LB, TB, wi, bi, si)])
@@ -313,7 +326,8 @@ class FluxTransformer2DModel:
                                    (LB, TB, self.R(p + "attn.to_out.0.weight"), self.R(p + "attn.to_out.0.bias"),
                                     self._site([p + "attn.to_out.0"]))])
             hx = O.GatedAddFn.apply(hx, ao, emb, st, [(0, LB, oc + 2 * D), (LB, TB, o + 2 * D)], B)
-            n2 = O.AdaLNFn.apply(hx, emb, st, [(0, LB, oc + 3 * D, oc + 4 * D), (LB, TB, o + 3 * D, o + 4 * D)], B)
+            n2, hx = _adaln_res(hx, emb, st, [(0, LB, oc + 3 * D, oc + 4 * D), (LB, TB, o + 3 * D, o + 4 * D)],
+                                        B)
             f1 = O.rows_linear(n2, [(0, LB, self.R(p + "ff_context.net.0.proj.weight"),
                                      self.R(p + "ff_context.net.0.proj.bias"), self._site([p + "ff_context.net.0.proj"])),
                                     (LB, TB, self.R(p + "ff.net.0.proj.weight"), self.R(p + "ff.net.0.proj.bias"),
@@ -329,7 +343,7 @@ class FluxTransformer2DModel:
         for j in range(cfg.num_single_layers):
             p = f"single_transformer_blocks.{j}."
             emb, st, o = mod[p + "norm.linear"]
-            n = O.AdaLNFn.apply(hx, emb, st, [(0, TB, o, o + D)], B)
+            n, hx = _adaln_res(hx, emb, st, [(0, TB, o, o + D)], B)
             wu, bu, su = self._fused_lin([p + "attn.to_q", p + "attn.to_k", p + "attn.to_v", p + "proj_mlp"], D)
             u = Fn.linear(n, wu, bu, lora=su)
             norms = (self.R(p + "attn.norm_q.weight"), self.R(p + "attn.norm_k.weight"), None, None)

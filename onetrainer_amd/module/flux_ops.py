@@ -134,6 +134,39 @@ class AdaLNFn(torch.autograd.Function):
         return dx, (ctx.state.d if ctx.owner else None), None, None, None
 
 
+class AdaLNResFn(torch.autograd.Function):
+    """(AdaLN(x), residual alias of x) for an adaLN whose input is also the block's residual (the gated add after the
+    attention / MLP branch): backward receives both gradient contributions and sums them inside the adaLN dx pass
+    (otamd_adaln_bwd_res) instead of leaving autograd a separate add."""
+
+    @staticmethod
+    def forward(ctx, x, emb, state, segs, B):
+        y = torch.empty_like(x)
+        stats = []
+        for r0, r1, sh, sc in segs:
+            _, st = K.adaln_fwd(x[r0:r1], emb, sh, sc, B, out=y[r0:r1])
+            stats.append(st)
+        ctx.save_for_backward(x, emb)
+        ctx.stats, ctx.state, ctx.segs, ctx.B = stats, state, segs, B
+        ctx.owner = state.claim()
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        x, emb = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(x)
+        if dy.stride(1) != 1:
+            dy = dy.contiguous()
+        if dres is not None and (dres.stride(1) != 1 or dres.stride(0) % 8):
+            dres = dres.contiguous()
+        dx = torch.empty_like(x)
+        for (r0, r1, sh, sc), st in zip(ctx.segs, ctx.stats):
+            K.adaln_bwd(x[r0:r1], dy[r0:r1], emb, sh, sc, ctx.B, st, dmod=ctx.state.d, dx=dx[r0:r1],
+                        dres=dres[r0:r1] if dres is not None else None)
+        return dx, (ctx.state.d if ctx.owner else None), None, None, None
+
+
 class GatedAddFn(torch.autograd.Function):
     """out[r0:r1] = x[r0:r1] + emb[b, gate_off:] * y[r0:r1] per row segment."""
 
