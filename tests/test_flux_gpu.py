@@ -41,6 +41,15 @@ def test_adaln_gated(dev):
     dx = K.adaln_bwd(x, dy, emb, 0, D, B, st, dmod=dmod)
     assert rel(dx, xr.grad.reshape(T * B, D)) < 2e-2
     assert rel(dmod[:, :2 * D], er.grad[:, :2 * D]) < 2e-2
+    # the residual gradient summed in the dx pass (otamd_adaln_bwd_res): rounded once, within one bf16 rounding of
+    # the separate add; the modulation gradients unchanged
+    dres = torch.randn(T * B, D, device=dev).bfloat16()
+    dmod2 = torch.zeros_like(emb)
+    dx2 = K.adaln_bwd(x, dy, emb, 0, D, B, st, dmod=dmod2, dres=dres)
+    ref2 = xr.grad.reshape(T * B, D) + dres.float()
+    assert rel(dx2, ref2) < 2e-2
+    assert (dx2.float() - (dx.float() + dres.float())).abs().max().item() <= 2 ** -7 * ref2.abs().max().item()
+    assert torch.equal(dmod2, dmod)
     # gated add: out = x + gate[b] * y
     yv = torch.randn(T * B, D, device=dev).bfloat16()
     out = K.gated_add_fwd(x, yv, emb, 2 * D, B)
