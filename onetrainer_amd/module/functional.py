@@ -72,6 +72,19 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
     return t.reshape(-1, t.shape[-1]) if t.is_contiguous() else t.view(-1, t.shape[-1])
 
 
+def _kernel_rows(t: torch.Tensor) -> bool:
+    """True when the kernels can read t in place as [rows, C] rows: unit channel stride, 16-byte aligned rows whose
+    leading dims collapse onto one row stride (e.g. a channel slice of the up path's concat gradient)."""
+    if t.stride(-1) != 1 or t.data_ptr() % 16 or t.dim() < 2 or t.stride(-2) % 8:
+        return False
+    exp = t.stride(-2)
+    for d in range(t.dim() - 2, -1, -1):
+        if t.shape[d] > 1 and t.stride(d) != exp:
+            return False
+        exp *= t.shape[d]
+    return True
+
+
 # ----------------------------------------------------------------------------------------------
 class LinearFn(torch.autograd.Function):
     """y = x @ W^T (+b) (+residual) over the last dim; x any [..., K] with unit inner stride."""
@@ -358,7 +371,7 @@ class GroupNormResFn(torch.autograd.Function):
     def backward(ctx, dy, dres):
         x, *stats = ctx.saved_tensors
         tr = ctx.gref.trainable
-        if dres is not None and (dres.stride(-1) != 1 or not dres.is_contiguous() or dres.data_ptr() % 16):
+        if dres is not None and not _kernel_rows(dres):   # strided rows (a concat-gradient slice) are read in place
             dres = dres.contiguous()
         if dy is None:   # only the residual use reached backward
             dy = torch.zeros_like(x)

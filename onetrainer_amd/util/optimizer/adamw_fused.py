@@ -304,13 +304,13 @@ class OverlappedGradNorm:
     def _on_ready(self, names):
         if not self.armed:
             return
-        from ...module import streams as S
-        side = S.side_stream()
+        pending, bucket_of = self.pending, self.bucket_of
         for n in names:
-            bi = self.bucket_of[n]
-            self.pending[bi] -= 1
-            if self.pending[bi] == 0 and not self.launched[bi]:
-                self._launch(bi, side)
+            bi = bucket_of[n]
+            pending[bi] -= 1
+            if pending[bi] == 0 and not self.launched[bi]:
+                from ...module import streams as S
+                self._launch(bi, S.side_stream())
 
     def finish(self):
         """after finish_backward (streams joined, grads of untouched tensors zeroed): sum what is left."""
