@@ -7,7 +7,8 @@ weights, same bf16-rounded inputs, same injected noise / timesteps):
   * SD 1.5 `sd15_config()` (8 heads of 40/80/160, ctx 768) at 512^2 b=1 -- C1's shape;
   * FLUX.1 at full width (D = 3072, 24 x 128 heads, T5 ctx 4096) with 1 double + 1 single block at
     768^2 b=1 (2304 image tokens + 77 text tokens).
-  * the SDXL UNet with C4's rank-32 LoRA on every Linear / Conv2d (oracle/lora.py hooks) at 512^2 b=1.
+  * the SDXL UNet with C4's rank-32 LoRA on every Linear / Conv2d (oracle/lora.py hooks) at 512^2 b=1, and the
+    full-width FLUX blocks with C5's rank-16 LoRA on every Linear at 768^2 b=1.
   Each checks the diffusion loss to rtol 1e-3 (north star), the prediction's element-wise cosine and every
   parameter (adapter) gradient's cosine.
 
@@ -193,6 +194,66 @@ def test_full_width_flux_blocks_768_match_oracle(dev):
     print("worst grad cosines:", cos[:4])
     assert cos[0][0] > 0.98, cos[:4]
     del m, om
+    _free()
+
+
+def test_full_width_flux_lora_blocks_768_match_oracle(dev):
+    """C5's adapter set at full width: FLUX (D = 3072, 1 double + 1 single block, frozen bf16 base) with rank-16 LoRA on
+    every Linear (module/lora.py: fused q|k|v(|mlp) downs, block-diagonal ups, second-K-segment GEMMs, the transposed
+    text / image row segments) against the oracle transformer with the reference LoRA hooks (oracle/lora.py,
+    LoRAModule.py:283-323) at 768^2 b=1: flow-matching loss to rtol 1e-3 and every adapter gradient's cosine."""
+    from onetrainer_amd.module.lora import LoRAWrapper
+    from oracle.lora import OracleLoRA
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    cfg = FX.FluxConfig(num_layers=1, num_single_layers=1)
+    ocfg = OF.FluxConfig(num_layers=1, num_single_layers=1)
+    m = FX.FluxTransformer2DModel(cfg, dev, seed=1, trainable=False)
+    with torch.device("meta"):
+        om = OF.FluxTransformer2DModel(ocfg)
+    om = om.to_empty(device="cpu")
+    om.load_state_dict({k: v.float().cpu() for k, v in m.state_dict().items()})
+    om.requires_grad_(False)
+    rank, alpha = 16, 16.0
+    lw = LoRAWrapper(m, rank=rank, alpha=alpha, prefix="lora_transformer", seed=0)
+    m.lora = lw
+    ol = OracleLoRA(om, rank, alpha, prefix="lora_transformer")
+    g = torch.Generator().manual_seed(5)
+    sd = {k: (torch.randn(v.shape, generator=g) * (0.01 if "lora_up" in k else 0.02) if not k.endswith(".alpha") else v)
+          for k, v in lw.state_dict().items()}
+    lw.load_state_dict(sd)
+    ol.load_state_dict({k: v for k, v in lw.state_dict().items() if not k.endswith(".alpha")})
+    B, h = 1, 96
+    lat = torch.randn(B, 16, h, h, generator=g)
+    eps = torch.randn(B, 16, h, h, generator=g)
+    t = torch.tensor([611], dtype=torch.int32)
+    pooled = torch.randn(B, 768, generator=g).bfloat16()
+    ehs = torch.randn(B, 77, 4096, generator=g).bfloat16()
+    x0 = (lat - 0.1159) * 0.3611
+    xt, _ = OD.add_noise_flow(x0, eps, t.long())
+    xin = xt.bfloat16().permute(0, 2, 3, 1).contiguous().to(dev)
+    tok = K.flux_pack(xin)
+    out_tok = m(tok, t.float().to(dev) / 1000, torch.ones(B, device=dev), pooled.to(dev), ehs.to(dev), h, h)
+    out = K.flux_unpack(out_tok.contiguous(), B, h, h, 16)
+    target = (eps - x0).permute(0, 2, 3, 1).contiguous().to(dev)
+    loss, coef, _ = K.mse_loss(out, target)
+    ref = om(OF.pack_latents(xt.bfloat16().float()), t.float() / 1000, torch.ones(B), pooled.float(), ehs.float(),
+             torch.zeros(77, 3), OF.prepare_latent_image_ids(h, h))
+    ref = OF.unpack_latents(ref, h, h)
+    ref_loss = OD.flow_matching_losses(ref, eps - x0, torch.ones(B)).mean()
+    print(f"flux lora r16 1+1 blocks 768^2 loss hip {loss.item():.6f} oracle {ref_loss.item():.6f}")
+    assert abs(loss.item() - ref_loss.item()) <= 1e-3 * abs(ref_loss.item())
+    lw.store.begin_backward()
+    d = K.mse_grad(out, target, coef)
+    out_tok.backward(K.flux_pack(d))
+    lw.store.finish_backward()
+    ref_loss.backward()
+    gs = lw.state_dict(grads=True)
+    assert set(gs) >= set(ol.params), sorted(set(ol.params) - set(gs))[:5]
+    cos = sorted((_cos(gs[k].float().cpu().reshape(p.shape), p.grad), k) for k, p in ol.params.items())
+    print(f"{len(cos)} adapter tensors; worst grad cosines:", cos[:4])
+    assert cos[0][0] > 0.98, cos[:4]
+    assert sum(c for c, _ in cos) / len(cos) > 0.999
+    del m, om, lw, ol
     _free()
 
 
