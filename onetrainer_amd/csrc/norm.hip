@@ -95,28 +95,28 @@ __global__ void __launch_bounds__(1024) gn_colreduce_kernel(const float* __restr
 }
 
 // fold channel sums into groups: mean / rstd per (n, g); a = rstd*gamma, b = beta - mean*a per (n, c).
-// sums: [N][2][C] double (sum x, sum x^2).  grid N, block 256
-__global__ void gn_finalize_kernel(const double* __restrict__ sums, int HW, int C, int G, float eps,
-                                   const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
-                                   float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ a_out,
-                                   float* __restrict__ b_out) {
-  const int n = blockIdx.x;
-  const int Cg = C / G;
+// sums: [N][2][C] double (sum x, sum x^2).  One wave per (group, image): the group's channel sums split over the
+// lanes and folded by a fixed xor butterfly (deterministic); grid (G, N).  The one-block-per-image form walked the
+// groups' channels serially (a dependent chain of global loads per group: 8.6 us per launch in the SDXL step).
+__global__ void __launch_bounds__(64) gn_finalize_g_kernel(const double* __restrict__ sums, int HW, int C, int G,
+                                                           float eps, const bf16_t* __restrict__ gamma,
+                                                           const bf16_t* __restrict__ beta, float* __restrict__ mean_out,
+                                                           float* __restrict__ rstd_out, float* __restrict__ a_out,
+                                                           float* __restrict__ b_out) {
+  const int g = blockIdx.x, n = blockIdx.y, lane = threadIdx.x;
+  const int Cg = C / G, c0 = g * Cg;
   const double* s = sums + (long long)n * 2 * C;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    double sm = 0, sq = 0;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { sm += s[c]; sq += s[C + c]; }
-    const double cnt = (double)HW * Cg;
-    const double mean = sm / cnt;
-    double var = sq / cnt - mean * mean;
-    if (var < 0) var = 0;
-    mean_out[n * G + g] = (float)mean;
-    rstd_out[n * G + g] = (float)(1.0 / sqrt(var + (double)eps));
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const int g = c / Cg;
-    const float m = mean_out[n * G + g], r = rstd_out[n * G + g];
+  double sm = 0, sq = 0;
+  for (int c = c0 + lane; c < c0 + Cg; c += 64) { sm += s[c]; sq += s[C + c]; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { sm += __shfl_xor(sm, o, 64); sq += __shfl_xor(sq, o, 64); }
+  const double cnt = (double)HW * Cg;
+  const double mean = sm / cnt;
+  double var = sq / cnt - mean * mean;
+  if (var < 0) var = 0;
+  const float m = (float)mean, r = (float)(1.0 / sqrt(var + (double)eps));
+  if (lane == 0) { mean_out[n * G + g] = m; rstd_out[n * G + g] = r; }
+  for (int c = c0 + lane; c < c0 + Cg; c += 64) {
     const float gm = gamma ? bf2f(gamma[c]) : 1.f;
     const float bt = beta ? bf2f(beta[c]) : 0.f;
     const float av = r * gm;
@@ -227,38 +227,32 @@ __global__ void __launch_bounds__(512) gn_bwd_reduce_kernel(const bf16_t* __rest
 // per (n, g) c1 = sum_c gamma S1 / cnt, c2 = sum_c gamma S2 / cnt from the block-summed
 // sums [N][2][C] (S1 = sum dz, S2 = sum dz xhat), folded into the apply coefficients
 // dx = A dz + B x + Cc with A = rstd gamma, B = -rstd^2 c2, Cc = rstd (mean rstd c2 - c1).
-// coef: [3][N][C] fp32.  grid N, block 256
-__global__ void gn_bwd_finalize_kernel(const double* __restrict__ sums, int N, int HW, int C, int G,
-                                       const bf16_t* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ rstd, float* __restrict__ coef) {
-  __shared__ float cc[2][256];
-  const int n = blockIdx.x;
-  const int Cg = C / G;
+// coef: [3][N][C] fp32.  One wave per (group, image), grid (G, N), as gn_finalize_g_kernel (the serial
+// one-block-per-image form took 13.9 us per launch)
+__global__ void __launch_bounds__(64) gn_bwd_finalize_g_kernel(const double* __restrict__ sums, int N, int HW, int C,
+                                                               int G, const bf16_t* __restrict__ gamma,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd, float* __restrict__ coef) {
+  const int g = blockIdx.x, n = blockIdx.y, lane = threadIdx.x;
+  const int Cg = C / G, c0 = g * Cg;
   const double* s1 = sums + (long long)n * 2 * C;
   const double* s2 = s1 + C;
-  for (int g0 = 0; g0 < G; g0 += 256) {
-    const int g = g0 + threadIdx.x;
-    if (g < G) {
-      double a = 0, q = 0;
-      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-        const double gm = gamma ? bf2f(gamma[c]) : 1.0;
-        a += gm * s1[c];
-        q += gm * s2[c];
-      }
-      cc[0][threadIdx.x] = (float)(a / ((double)HW * Cg));
-      cc[1][threadIdx.x] = (float)(q / ((double)HW * Cg));
-    }
-    __syncthreads();
-    for (int c = g0 * Cg + threadIdx.x; c < min(G, g0 + 256) * Cg; c += blockDim.x) {
-      const int gi = c / Cg - g0, ng = n * G + g0 + gi;
-      const float r = rstd[ng], m = mean[ng];
-      const float c1 = cc[0][gi], c2 = cc[1][gi];
-      const float gm = gamma ? bf2f(gamma[c]) : 1.f;
-      coef[(long long)n * C + c] = r * gm;
-      coef[(long long)(N + n) * C + c] = -r * r * c2;
-      coef[(long long)(2 * N + n) * C + c] = r * (m * r * c2 - c1);
-    }
-    __syncthreads();
+  double a = 0, q = 0;
+  for (int c = c0 + lane; c < c0 + Cg; c += 64) {
+    const double gm = gamma ? bf2f(gamma[c]) : 1.0;
+    a += gm * s1[c];
+    q += gm * s2[c];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); q += __shfl_xor(q, o, 64); }
+  const float c1 = (float)(a / ((double)HW * Cg)), c2 = (float)(q / ((double)HW * Cg));
+  const int ng = n * G + g;
+  const float r = rstd[ng], m = mean[ng];
+  for (int c = c0 + lane; c < c0 + Cg; c += 64) {
+    const float gm = gamma ? bf2f(gamma[c]) : 1.f;
+    coef[(long long)n * C + c] = r * gm;
+    coef[(long long)(N + n) * C + c] = -r * r * c2;
+    coef[(long long)(2 * N + n) * C + c] = r * (m * r * c2 - c1);
   }
 }
 
@@ -366,8 +360,8 @@ OTAMD_API int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long lo
   double* sums = reinterpret_cast<double*>(ws + (long long)N * grid.x * 2 * C + 3LL * N * C + ((3LL * N * C) & 1));
   gn_colreduce_kernel<<<dim3((2 * C + 63) / 64, N), 1024, 0, stream>>>(ws, grid.x, 2 * C, sums);
   OTAMD_CHECK_LAUNCH();
-  gn_finalize_kernel<<<N, 256, 0, stream>>>(sums, HW, C, G, eps, (const bf16_t*)gamma, (const bf16_t*)beta, mean, rstd,
-                                            a, b);
+  gn_finalize_g_kernel<<<dim3(G, N), 64, 0, stream>>>(sums, HW, C, G, eps, (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                      mean, rstd, a, b);
   OTAMD_CHECK_LAUNCH();
   if (silu) gn_apply_kernel<true><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, HW, C, ppb, a, b);
   else gn_apply_kernel<false><<<grid, nt, 0, stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, HW, C, ppb, a, b);
@@ -403,7 +397,7 @@ static int groupnorm_bwd_impl(const void* x, long long ldx, const void* dy, long
   OTAMD_CHECK_LAUNCH();
   gn_colreduce_kernel<<<dim3((2 * C + 63) / 64, N), 1024, 0, stream>>>(part, grid.x, 2 * C, sums);
   OTAMD_CHECK_LAUNCH();
-  gn_bwd_finalize_kernel<<<N, 256, 0, stream>>>(sums, N, HW, C, G, (const bf16_t*)gamma, mean, rstd, coef);
+  gn_bwd_finalize_g_kernel<<<dim3(G, N), 64, 0, stream>>>(sums, N, HW, C, G, (const bf16_t*)gamma, mean, rstd, coef);
   OTAMD_CHECK_LAUNCH();
   if (dgamma || dbeta) {
     gn_param_grad_kernel<<<(C + 255) / 256, 256, 0, stream>>>(sums, N, C, dgamma, dbeta, param_f32, param_acc);
