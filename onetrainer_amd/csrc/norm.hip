@@ -73,23 +73,24 @@ __global__ void __launch_bounds__(512) gn_stats_kernel(const bf16_t* __restrict_
 }
 
 // sum the per-block partial slabs over blocks in double: out[n][i] = sum_blk part[n][blk][i], i < 2C.
-// grid (ceil(2C / 64), N), block 1024 = 64 columns x 16 partial lanes (coalesced column reads)
+// grid (ceil(2C / 16), N), block 1024 = 16 columns x 64 partial lanes: lane p sums blocks p, p + 64, ... (a few loads
+// in flight each), the 64 partials are folded in lane order (deterministic).  (64 columns x 16 lanes ran 16
+// dependent iterations per lane over ~40 blocks: 8.4 us per launch in the SDXL step.)
 __global__ void __launch_bounds__(1024) gn_colreduce_kernel(const float* __restrict__ part, int nblk, int C2,
                                                             double* __restrict__ out) {
-  __shared__ double red[16][65];
-  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
-  const int n = blockIdx.y, i = blockIdx.x * 64 + cl;
+  __shared__ double red[64][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int n = blockIdx.y, i = blockIdx.x * 16 + cl;
   double s = 0.0;
   if (i < C2) {
     const float* pb = part + (long long)n * nblk * C2 + i;
-    for (int blk = pl; blk < nblk; blk += 16) s += pb[(long long)blk * C2];
+    for (int blk = pl; blk < nblk; blk += 64) s += pb[(long long)blk * C2];
   }
   red[pl][cl] = s;
   __syncthreads();
   if (pl == 0 && i < C2) {
     double t = 0.0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    for (int k = 0; k < 64; ++k) t += red[k][cl];
     out[(long long)n * C2 + i] = t;
   }
 }
@@ -358,7 +359,7 @@ OTAMD_API int otamd_groupnorm_fwd(const void* x, long long ldx, void* y, long lo
   gn_stats_kernel<<<grid, nt, ppp * 2 * C * sizeof(float), stream>>>((const bf16_t*)x, ldx, HW, C, ppb, ws);
   OTAMD_CHECK_LAUNCH();
   double* sums = reinterpret_cast<double*>(ws + (long long)N * grid.x * 2 * C + 3LL * N * C + ((3LL * N * C) & 1));
-  gn_colreduce_kernel<<<dim3((2 * C + 63) / 64, N), 1024, 0, stream>>>(ws, grid.x, 2 * C, sums);
+  gn_colreduce_kernel<<<dim3((2 * C + 15) / 16, N), 1024, 0, stream>>>(ws, grid.x, 2 * C, sums);
   OTAMD_CHECK_LAUNCH();
   gn_finalize_g_kernel<<<dim3(G, N), 64, 0, stream>>>(sums, HW, C, G, eps, (const bf16_t*)gamma, (const bf16_t*)beta,
                                                       mean, rstd, a, b);
@@ -395,7 +396,7 @@ static int groupnorm_bwd_impl(const void* x, long long ldx, const void* dy, long
     gn_bwd_reduce_kernel<false><<<grid, nt, ppp * 2 * C * sizeof(float), stream>>>(
         (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, HW, C, G, ppb, a, b, mean, rstd, part);
   OTAMD_CHECK_LAUNCH();
-  gn_colreduce_kernel<<<dim3((2 * C + 63) / 64, N), 1024, 0, stream>>>(part, grid.x, 2 * C, sums);
+  gn_colreduce_kernel<<<dim3((2 * C + 15) / 16, N), 1024, 0, stream>>>(part, grid.x, 2 * C, sums);
   OTAMD_CHECK_LAUNCH();
   gn_bwd_finalize_g_kernel<<<dim3(G, N), 64, 0, stream>>>(sums, N, HW, C, G, (const bf16_t*)gamma, mean, rstd, coef);
   OTAMD_CHECK_LAUNCH();
@@ -928,22 +929,23 @@ static int ln_pick(int C8, int* L) {
   return 0;
 }
 
-// sum block partials [nb][2][C] -> dgamma, dbeta: 64 columns x 16 partial lanes per block
+// sum block partials [nb][2][C] -> dgamma, dbeta: 16 columns x 64 partial lanes per block (as gn_colreduce_kernel:
+// a few loads in flight per lane, the partials folded in lane order; 64 x 16 ran up to 32 dependent iterations per
+// lane over 40 blocks, 5.4 us per launch in the SDXL step)
 __global__ void __launch_bounds__(1024) ln_param_reduce2_kernel(const float* __restrict__ part, int nb, int C,
                                                                 void* __restrict__ dgamma, void* __restrict__ dbeta,
                                                                 int pf32, int pacc) {
-  __shared__ float red[16][65];
-  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float red[64][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float s = 0.f;
   if (c < 2 * C)
-    for (int b = pl; b < nb; b += 16) s += part[(long long)b * 2 * C + c];
+    for (int b = pl; b < nb; b += 64) s += part[(long long)b * 2 * C + c];
   red[pl][cl] = s;
   __syncthreads();
   if (pl == 0 && c < 2 * C) {
     float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    for (int k = 0; k < 64; ++k) t += red[k][cl];
     if (c < C) store_param_grad(dgamma, c, t, pf32, pacc); else store_param_grad(dbeta, c - C, t, pf32, pacc);
   }
 }
@@ -1080,7 +1082,7 @@ OTAMD_API int otamd_layernorm_bwd_fused(const void* x, long long ldx, const void
 #undef LNBF
   if (!launched) return OTAMD_EUNSUPPORTED;
   OTAMD_CHECK_LAUNCH();
-  ln_param_reduce2_kernel<<<(2 * C + 63) / 64, 1024, 0, stream>>>(part, nb, C, dgamma, dbeta, param_f32, param_acc);
+  ln_param_reduce2_kernel<<<(2 * C + 15) / 16, 1024, 0, stream>>>(part, nb, C, dgamma, dbeta, param_f32, param_acc);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
@@ -1144,7 +1146,7 @@ static int ln_param_grads(const void* x, long long ldx, const void* dy, long lon
     ln_param_part_kernel<<<dim3(cb, slabs), 512, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, rows, C,
                                                               mean, rstd, rps, part);
     OTAMD_CHECK_LAUNCH();
-    ln_param_reduce2_kernel<<<(2 * C + 63) / 64, 1024, 0, stream>>>(part, slabs, C, dgamma, dbeta, param_f32, param_acc);
+    ln_param_reduce2_kernel<<<(2 * C + 15) / 16, 1024, 0, stream>>>(part, slabs, C, dgamma, dbeta, param_f32, param_acc);
     OTAMD_CHECK_LAUNCH();
     return OTAMD_OK;
   }
