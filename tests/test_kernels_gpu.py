@@ -230,8 +230,10 @@ def test_silu_concat_pool_colsum(dev):
     m = rnd(2 * 4096, 320, dev=dev)
     cs = K.colsum(m, 4096)
     assert rel_err(cs, m.float().view(2, 4096, 320).sum(1)) < 1e-3
+    m = rnd(4 * 16384, 320, dev=dev)   # SDXL level-1 per-image drow shape
+    assert rel_err(K.colsum(m, 16384), m.float().view(4, 16384, 320).sum(1)) < 1e-3
     # ragged row counts (unroll tail), wide rows, a strided column slice, fp32 accumulate
-    for rows, cols in ((1, 8), (77, 2048), (16384 + 40, 640), (4096 * 3 + 7, 10240)):
+    for rows, cols in ((1, 8), (9, 24), (77, 2048), (16384 + 40, 640), (3005, 1280), (4096 * 3 + 7, 10240)):
         m = rnd(rows, cols, dev=dev)
         assert rel_err(K.colsum(m), m.float().sum(0, keepdim=True)) < 1e-3, (rows, cols)
     big = rnd(5000, 1920, dev=dev)
