@@ -256,6 +256,18 @@ int otamd_layernorm_param_grad(const void* x, long long ldx, const void* dy, lon
     const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32, int param_acc, float* part,
     hipStream_t stream);
 
+/* Deferred LayerNorm parameter reduces: while a stream is in defer mode, otamd_layernorm_param_grad (and
+   otamd_layernorm_bwd with parameter gradients) on it write their per-slab partials into `arena` and leave the final
+   dgamma / dbeta sums pending; one grouped launch sums up to 64 of them (bit-identical to the immediate path).  The
+   caller flushes before anything reads those gradients (the gradient-norm / DP bucket launches, the end of backward).
+   Reference: the gamma / beta gradients of diffusers' BasicTransformerBlock norm1-3 (replaces nothing in the
+   reference's own code: torch's fused LayerNorm backward reduces them inside one kernel). */
+int otamd_layernorm_defer_begin(hipStream_t stream, void* arena, long long bytes);
+int otamd_layernorm_defer_flush(hipStream_t stream);
+int otamd_layernorm_defer_end(hipStream_t stream);
+/* out[0] LayerNorms deferred, out[1] grouped launches (totals since load), out[2] pending on `stream` */
+int otamd_layernorm_defer_stats(hipStream_t stream, long long* out);
+
 /* replaces: diffusers GEGLU (ff.net.0) hidden * gelu(gate) */
 int otamd_geglu_fwd(const void* h, long long ldh, void* out, long long ldo, int M, int F, hipStream_t s);
 

@@ -102,6 +102,10 @@ SIGNATURES: dict[str, list] = {
     "otamd_layernorm_fwd": [VP, LL, VP, LL, I, I, F, VP, VP, VP, VP, VP],
     "otamd_layernorm_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],
     "otamd_layernorm_param_grad": [VP, LL, VP, LL, I, I, VP, VP, VP, VP, I, I, VP, VP],
+    "otamd_layernorm_defer_begin": [VP, VP, LL],
+    "otamd_layernorm_defer_flush": [VP],
+    "otamd_layernorm_defer_end": [VP],
+    "otamd_layernorm_defer_stats": [VP, VP],
     "otamd_layernorm_bwd_res": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP],
     "otamd_layernorm_bwd_fused": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],
     # attention.hip

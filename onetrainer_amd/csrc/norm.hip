@@ -13,6 +13,8 @@
 #include "common.h"
 
 #include <stdlib.h>
+#include <mutex>
+#include <unordered_map>
 
 __device__ __forceinline__ void store_param_grad(void* p, long long i, float v, int f32, int acc);
 
@@ -932,12 +934,12 @@ static int ln_pick(int C8, int* L) {
 // sum block partials [nb][2][C] -> dgamma, dbeta: 16 columns x 64 partial lanes per block (as gn_colreduce_kernel:
 // a few loads in flight per lane, the partials folded in lane order; 64 x 16 ran up to 32 dependent iterations per
 // lane over 40 blocks, 5.4 us per launch in the SDXL step)
-__global__ void __launch_bounds__(1024) ln_param_reduce2_kernel(const float* __restrict__ part, int nb, int C,
-                                                                void* __restrict__ dgamma, void* __restrict__ dbeta,
-                                                                int pf32, int pacc) {
+__device__ __forceinline__ void ln_param_reduce_body(const float* __restrict__ part, int nb, int C,
+                                                     void* __restrict__ dgamma, void* __restrict__ dbeta, int pf32,
+                                                     int pacc, int bx) {
   __shared__ float red[64][17];
   const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  const int c = bx * 16 + cl;
   float s = 0.f;
   if (c < 2 * C)
     for (int b = pl; b < nb; b += 64) s += part[(long long)b * 2 * C + c];
@@ -948,6 +950,122 @@ __global__ void __launch_bounds__(1024) ln_param_reduce2_kernel(const float* __r
     for (int k = 0; k < 64; ++k) t += red[k][cl];
     if (c < C) store_param_grad(dgamma, c, t, pf32, pacc); else store_param_grad(dbeta, c - C, t, pf32, pacc);
   }
+}
+
+__global__ void __launch_bounds__(1024) ln_param_reduce2_kernel(const float* __restrict__ part, int nb, int C,
+                                                                void* __restrict__ dgamma, void* __restrict__ dbeta,
+                                                                int pf32, int pacc) {
+  ln_param_reduce_body(part, nb, C, dgamma, dbeta, pf32, pacc, blockIdx.x);
+}
+
+// ---- deferred LayerNorm parameter reduces (otamd_layernorm_defer_*) ----------------------------------------------
+// dgamma / dbeta only feed the optimizer, so on a deferring stream the parameter-gradient pass writes its per-slab
+// partials into a caller-owned arena and the final sums of up to kLnMaxDefer LayerNorms go out in one grouped launch
+// (each LayerNorm's columns summed exactly as ln_param_reduce2_kernel sums them: bit-identical).  210 reduce launches
+// of ~5 us each per SDXL 1024^2 step otherwise sit on the critical stream.
+struct LnDeferDesc {
+  const float* part; void* dg; void* db;
+  int nb, C, flags;   // flags: 1 fp32 destinations, 2 accumulate
+  unsigned block0;
+};
+constexpr int kLnMaxDefer = 64;
+struct LnDeferBatch { int n; unsigned blocks; LnDeferDesc d[kLnMaxDefer]; };
+
+__global__ void __launch_bounds__(1024) ln_param_reduce_grouped_kernel(LnDeferBatch bt) {
+  int i = 0;
+  while (i + 1 < bt.n && blockIdx.x >= bt.d[i + 1].block0) ++i;
+  const LnDeferDesc& d = bt.d[i];
+  ln_param_reduce_body(d.part, d.nb, d.C, d.dg, d.db, d.flags & 1, (d.flags >> 1) & 1, blockIdx.x - d.block0);
+}
+
+struct LnDeferState {
+  char* arena = nullptr;
+  long long bytes = 0, used = 0;
+  LnDeferBatch batch{};
+};
+static std::mutex g_ln_defer_mu;
+static std::unordered_map<hipStream_t, LnDeferState> g_ln_defer;
+static long long g_ln_defer_norms = 0, g_ln_defer_launches = 0;
+
+static void ln_defer_flush_locked(LnDeferState& st, hipStream_t stream) {
+  if (st.batch.n > 0) {
+    ln_param_reduce_grouped_kernel<<<st.batch.blocks, 1024, 0, stream>>>(st.batch);
+    g_ln_defer_norms += st.batch.n;
+    ++g_ln_defer_launches;
+    st.batch.n = 0;
+    st.batch.blocks = 0;
+  }
+  st.used = 0;
+}
+
+// partial slab memory for one LayerNorm's parameter pass on a deferring stream (nullptr: not deferring, or the
+// partials do not fit the arena).  A pending reduce into the same dgamma / dbeta is flushed first (two grouped
+// reduces of one destination would race).
+static float* ln_defer_slot(long long need, const void* dg, const void* db, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_ln_defer_mu);
+  auto it = g_ln_defer.find(stream);
+  if (it == g_ln_defer.end()) return nullptr;
+  LnDeferState& st = it->second;
+  need = (need + 255) / 256 * 256;
+  if (need > st.bytes) return nullptr;
+  bool clash = false;
+  for (int i = 0; i < st.batch.n && !clash; ++i) clash = st.batch.d[i].dg == dg || st.batch.d[i].db == db;
+  if (clash || st.batch.n == kLnMaxDefer || st.used + need > st.bytes) ln_defer_flush_locked(st, stream);
+  float* p = reinterpret_cast<float*>(st.arena + st.used);
+  st.used += need;
+  return p;
+}
+
+static void ln_defer_record(const float* part, int nb, int C, void* dg, void* db, int f32, int acc,
+                            hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_ln_defer_mu);
+  LnDeferState& st = g_ln_defer[stream];
+  LnDeferDesc& d = st.batch.d[st.batch.n++];
+  d.part = part; d.dg = dg; d.db = db; d.nb = nb; d.C = C; d.flags = (f32 ? 1 : 0) | (acc ? 2 : 0);
+  d.block0 = st.batch.blocks;
+  st.batch.blocks += (unsigned)((2 * C + 15) / 16);
+}
+
+// start deferring this stream's LayerNorm parameter reduces into `arena` (>= 1 MiB, 256-byte aligned, kept alive by
+// the caller until otamd_layernorm_defer_end); reduces pending from an earlier begin are flushed first
+OTAMD_API int otamd_layernorm_defer_begin(hipStream_t stream, void* arena, long long bytes) {
+  if (!arena || ((uintptr_t)arena & 255) || bytes < (1 << 20)) return OTAMD_EINVAL;
+  std::lock_guard<std::mutex> lk(g_ln_defer_mu);
+  LnDeferState& st = g_ln_defer[stream];
+  ln_defer_flush_locked(st, stream);
+  st.arena = (char*)arena;
+  st.bytes = bytes;
+  st.used = 0;
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+// launch the grouped reduce of every pending LayerNorm on this stream (stream-ordered); a no-op when none is pending
+OTAMD_API int otamd_layernorm_defer_flush(hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_ln_defer_mu);
+  auto it = g_ln_defer.find(stream);
+  if (it != g_ln_defer.end()) ln_defer_flush_locked(it->second, stream);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+// flush and leave defer mode
+OTAMD_API int otamd_layernorm_defer_end(hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_ln_defer_mu);
+  auto it = g_ln_defer.find(stream);
+  if (it == g_ln_defer.end()) return OTAMD_OK;
+  ln_defer_flush_locked(it->second, stream);
+  g_ln_defer.erase(it);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+// out[0] = LayerNorms whose parameter reduce went out deferred, out[1] = grouped launches, out[2] = pending on stream
+OTAMD_API int otamd_layernorm_defer_stats(hipStream_t stream, long long* out) {
+  if (!out) return OTAMD_EINVAL;
+  std::lock_guard<std::mutex> lk(g_ln_defer_mu);
+  out[0] = g_ln_defer_norms;
+  out[1] = g_ln_defer_launches;
+  auto it = g_ln_defer.find(stream);
+  out[2] = it == g_ln_defer.end() ? 0 : it->second.batch.n;
+  return OTAMD_OK;
 }
 
 static int ln_param_grads(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,
@@ -1143,9 +1261,14 @@ static int ln_param_grads(const void* x, long long ldx, const void* dy, long lon
     slabs = min(slabs, 512);
     const int rps = (rows + slabs - 1) / slabs;
     slabs = (rows + rps - 1) / rps;
+    float* dpart = ln_defer_slot((long long)slabs * 2 * C * sizeof(float), dgamma, dbeta, stream);
     ln_param_part_kernel<<<dim3(cb, slabs), 512, 0, stream>>>((const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, rows, C,
-                                                              mean, rstd, rps, part);
+                                                              mean, rstd, rps, dpart ? dpart : part);
     OTAMD_CHECK_LAUNCH();
+    if (dpart) {
+      ln_defer_record(dpart, slabs, C, dgamma, dbeta, param_f32, param_acc, stream);
+      return OTAMD_OK;
+    }
     ln_param_reduce2_kernel<<<(2 * C + 15) / 16, 1024, 0, stream>>>(part, slabs, C, dgamma, dbeta, param_f32, param_acc);
     OTAMD_CHECK_LAUNCH();
     return OTAMD_OK;

@@ -91,6 +91,36 @@ def defer_reduces_pending(stream) -> int:
     return int(lib().otamd_gemm_defer_pending(C.c_void_p(stream.cuda_stream)))
 
 
+_LN_DEFER_ARENAS: dict = {}
+
+
+def ln_defer_begin(stream, nbytes: int = 64 << 20) -> None:
+    """defer the LayerNorm parameter-gradient reduces launched on `stream` (a torch Stream): their per-slab partials
+    go to an arena and up to 64 LayerNorms' final dgamma / dbeta sums go out in one grouped launch
+    (otamd_layernorm_defer_begin: bit-identical)"""
+    key = stream.cuda_stream
+    ar = _LN_DEFER_ARENAS.get(key)
+    if ar is None or ar.numel() < nbytes:
+        ar = _LN_DEFER_ARENAS[key] = torch.empty(nbytes, dtype=torch.uint8, device=stream.device)
+    check(lib().otamd_layernorm_defer_begin(C.c_void_p(key), _p(ar), ar.numel()), "otamd_layernorm_defer_begin")
+
+
+def ln_defer_flush(stream) -> None:
+    check(lib().otamd_layernorm_defer_flush(C.c_void_p(stream.cuda_stream)), "otamd_layernorm_defer_flush")
+
+
+def ln_defer_end(stream) -> None:
+    check(lib().otamd_layernorm_defer_end(C.c_void_p(stream.cuda_stream)), "otamd_layernorm_defer_end")
+
+
+def ln_defer_stats(stream) -> tuple:
+    """(LayerNorms whose parameter reduce went out deferred, grouped launches, pending on `stream`)"""
+    out = (C.c_longlong * 3)()
+    check(lib().otamd_layernorm_defer_stats(C.c_void_p(stream.cuda_stream), C.cast(out, C.c_void_p)),
+          "otamd_layernorm_defer_stats")
+    return int(out[0]), int(out[1]), int(out[2])
+
+
 _gemm_forced_splits = 0   # tools/gemm_splits.py probe: forces the split count of planned GEMMs
 
 # ---- GEMM plan autotuner --------------------------------------------------------------------

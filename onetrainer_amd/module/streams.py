@@ -116,19 +116,33 @@ def note_side(tensors, depth: int = 1):
 
 
 _DEFER = os.environ.get("OTAMD_DEFER_REDUCE", "1") != "0"
+_LN_DEFER = os.environ.get("OTAMD_LN_DEFER", "1") != "0"
+_LN_STREAM: list = []   # the stream whose LayerNorm parameter reduces are deferred (kernels.ln_defer_begin)
 
 
 def defer_begin(grads):
     """start of a backward: the side stream's split-K reduces into the flat gradient buffer `grads` are deferred and
-    launched grouped (kernels.defer_reduces_begin; OTAMD_DEFER_REDUCE=0 launches each with its GEMM)"""
+    launched grouped (kernels.defer_reduces_begin; OTAMD_DEFER_REDUCE=0 launches each with its GEMM), and so are the
+    current stream's LayerNorm dgamma / dbeta reduces (kernels.ln_defer_begin; OTAMD_LN_DEFER=0 launches each with
+    its LayerNorm)"""
+    if grads is None or not grads.numel():
+        return
+    from .. import kernels as K
     side = side_stream()
-    if side is not None and _DEFER and grads is not None and grads.numel():
-        from .. import kernels as K
+    if side is not None and _DEFER:
         K.defer_reduces_begin(side, grads)
+    if _LN_DEFER and enabled():
+        main = _current(grads.device.index)
+        K.ln_defer_begin(main)
+        _LN_STREAM[:] = [main]
 
 
 def defer_flush():
-    """before anything reads weight gradients the side stream produced (norm chunks, DP buckets, the join)"""
+    """before anything reads weight gradients the side stream produced (norm chunks, DP buckets, the join) -- called
+    on the main stream, so the LayerNorm reduces flushed here are ordered before the reader's fork event"""
+    if _LN_STREAM:
+        from .. import kernels as K
+        K.ln_defer_flush(_LN_STREAM[0])
     side = side_stream()
     if side is not None and _DEFER:
         from .. import kernels as K
@@ -136,6 +150,9 @@ def defer_flush():
 
 
 def defer_end():
+    if _LN_STREAM:
+        from .. import kernels as K
+        K.ln_defer_end(_LN_STREAM.pop())
     side = side_stream()
     if side is not None and _DEFER:
         from .. import kernels as K

@@ -97,10 +97,12 @@ class GradBucketReducer:
             self.works.append((self._reduce(g, b, e), bi))
             return
         s = self.issue_stream
+        # the deferred reduces write into this bucket: the side stream's split-K ones and this stream's LayerNorm
+        # parameter ones (module/streams.py), flushed before the wait below orders the collective after them
+        S.defer_flush()
         s.wait_stream(torch.cuda.current_stream())
         side = S.side_stream()
         if side is not None:
-            S.defer_flush()   # the deferred split-K reduces of the side stream write into this bucket
             s.wait_stream(side)
         with torch.cuda.stream(s):
             self.works.append((self._reduce(g, b, e), bi))

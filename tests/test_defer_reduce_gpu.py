@@ -3,7 +3,8 @@
 The LoRA adapter gradients are split-K GEMMs (rank-wide outputs, K = tokens); deferring their reduces and launching
 them grouped must not change a bit: each output is still summed in split order.  Checked on whole backward passes
 (overwrite and gradient-accumulation micro-steps) of the tiny SDXL LoRA and the full-width SDXL LoRA r32 at 512^2,
-b=1 (the C4 bench configuration), plus the flush-before-read guard on a direct GEMM chain.
+b=1 (the C4 bench configuration), plus the flush-before-read guard on a direct GEMM chain.  The LayerNorm parameter reduces (otamd_layernorm_defer_*) are
+deferred the same way on the main stream: checked on full fine-tune steps of the tiny SDXL UNet and at SDXL 512^2.
 """
 import copy
 
@@ -104,3 +105,69 @@ def test_defer_flushes_before_dependent_gemm(dev):
     torch.cuda.synchronize()
     assert torch.equal(w1, ref1) and torch.equal(outside, ref1)
     assert torch.equal(z, K.linear_dgrad(y2, ref1))
+
+
+def _ft_trainer(dev, ucfg):
+    cfg = TrainConfig.default_values()
+    cfg.batch_size = 1
+    cfg.learning_rate_warmup_steps = 0
+    cfg.gradient_accumulation_steps = 1000
+    model = create.create_model(cfg, dev, seed=5, unet_config=ucfg)
+    tr = GenericTrainer(cfg, model=model)
+    tr.start()
+    return tr
+
+
+@pytest.mark.parametrize("which", ["tiny", "sdxl_512"])
+def test_deferred_layernorm_param_reduces_bit_identical(dev, which, monkeypatch):
+    if which == "tiny":
+        tr = _ft_trainer(dev, U.tiny_sdxl_config())
+        batch = synthetic_sdxl_batch(1, 256, 256, dev, seed=0, te1_dim=48, te2_dim=48, pooled_dim=64)
+    else:
+        tr = _ft_trainer(dev, None)
+        batch = synthetic_sdxl_batch(1, 512, 512, dev, seed=0)
+    tr.train_step(batch)
+    torch.cuda.synchronize()
+    tr.model.train_store.accumulating = False
+    monkeypatch.setattr(S, "_LN_DEFER", False)
+    ref = _two_microsteps(tr, batch, True, monkeypatch)
+    monkeypatch.setattr(S, "_LN_DEFER", True)
+    main = torch.cuda.current_stream()
+    n0, l0, _ = K.ln_defer_stats(main)
+    got = _two_microsteps(tr, batch, True, monkeypatch)
+    n1, l1, pending = K.ln_defer_stats(main)
+    assert pending == 0
+    deferred, launches = n1 - n0, l1 - l0
+    assert deferred > 0 and launches > 0 and launches * 2 <= deferred, (deferred, launches)
+    for (la, ga), (lb, gb) in zip(ref, got):
+        assert torch.equal(la, lb)
+        assert torch.equal(ga, gb), (ga.float() - gb.float()).abs().max().item()
+    assert not torch.equal(ref[0][1], ref[1][1])
+    print(f"{which}: {deferred // 2} LayerNorm parameter reduces in {launches // 2} grouped launches per backward")
+
+
+def test_layernorm_defer_flush_order(dev):
+    """a pending reduce into the same dgamma is flushed before the next one is recorded (accumulation stays ordered);
+    flush / end leave nothing pending and the sums equal the immediate path's"""
+    g = torch.Generator(device=dev).manual_seed(3)
+    BF = torch.bfloat16
+    x = torch.randn(4096, 1280, device=dev, generator=g).to(BF)
+    dy = torch.randn(4096, 1280, device=dev, generator=g).to(BF)
+    gamma = torch.ones(1280, device=dev, dtype=BF)
+    beta = torch.zeros(1280, device=dev, dtype=BF)
+    _, stats = K.layernorm_fwd(x, gamma, beta, 1e-5)
+    dg0, db0 = torch.zeros(1280, device=dev), torch.zeros(1280, device=dev)
+    K.layernorm_param_grad(x, dy, stats, dg0, db0)
+    K.layernorm_param_grad(x, dy, stats, dg0, db0, param_acc=True)
+    main = torch.cuda.current_stream()
+    dg, db = torch.zeros(1280, device=dev), torch.zeros(1280, device=dev)
+    K.ln_defer_begin(main)
+    K.layernorm_param_grad(x, dy, stats, dg, db)
+    assert K.ln_defer_stats(main)[2] == 1
+    K.layernorm_param_grad(x, dy, stats, dg, db, param_acc=True)   # same destination: the first is flushed
+    assert K.ln_defer_stats(main)[2] == 1
+    K.ln_defer_flush(main)
+    assert K.ln_defer_stats(main)[2] == 0
+    K.ln_defer_end(main)
+    torch.cuda.synchronize()
+    assert torch.equal(dg, dg0) and torch.equal(db, db0)
