@@ -39,8 +39,9 @@ __global__ void geglu_bwd_kernel(const bf16_t* __restrict__ h, long long ldh, co
     unpack8(*reinterpret_cast<const bf8*>(dout + m * lddo + c), d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      da[j] = d[j] * gelu_f(g[j]);
-      dg[j] = d[j] * a[j] * dgelu_f(g[j]);
+      const GeluTerms t = gelu_terms(g[j]);
+      da[j] = d[j] * g[j] * t.cdf;                      // d * gelu(g)
+      dg[j] = d[j] * a[j] * fmaf(g[j], t.pdf, t.cdf);   // d * a * gelu'(g)
     }
     *reinterpret_cast<bf8*>(dh + m * lddh + c) = pack8(da);
     *reinterpret_cast<bf8*>(dh + m * lddh + F + c) = pack8(dg);
