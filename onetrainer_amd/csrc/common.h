@@ -81,9 +81,9 @@ __device__ __forceinline__ GeluTerms gelu_terms(float x) {
   const float poly =
       t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
   const float e = __expf(-z * z);
-  const float erf_abs = fmaf(-poly, e, 1.f);
+  const float tail = 0.5f * poly * e;   // 0.5 erfc(|z|): Phi(-|x|), taken directly (no 1 - erf cancellation)
   GeluTerms r;
-  r.cdf = 0.5f * (1.f + copysignf(erf_abs, x));
+  r.cdf = x < 0.f ? tail : 1.f - tail;
   r.pdf = 0.39894228040143268f * e;
   return r;
 }

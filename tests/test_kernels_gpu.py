@@ -212,6 +212,19 @@ def test_geglu(dev):
     do = rnd(300, 2560, dev=dev)
     ref.backward(do.float())
     assert rel_err(K.geglu_bwd(h, do), hr.grad) < 1e-2
+    # GELU's erf is the Abramowitz-Stegun 7.1.26 form (common.h, |erf error| <= 1.5e-7): gates over the whole range,
+    # both tails and 0, element-wise against fp64 erf within bf16 rounding of the outputs + 1e-6 absolute (the
+    # negative tail, where torch's own fp32 0.5 (1 + erf) loses its relative accuracy too)
+    g = torch.linspace(-12, 12, 2560 * 8, device=dev).view(8, 2560)
+    h2 = torch.cat([torch.ones_like(g), g], dim=-1).to(BF)
+    gq = h2[:, 2560:].double()
+    gelu = 0.5 * gq * (1 + torch.erf(gq / math.sqrt(2)))
+    dgelu = 0.5 * (1 + torch.erf(gq / math.sqrt(2))) + gq * torch.exp(-0.5 * gq * gq) / math.sqrt(2 * math.pi)
+    y2 = K.geglu_fwd(h2).double()
+    assert ((y2 - gelu).abs() <= 2 ** -8 * gelu.abs() + 1e-6).all()
+    d2 = K.geglu_bwd(h2, torch.ones(8, 2560, device=dev, dtype=BF)).double()
+    assert ((d2[:, :2560] - gelu).abs() <= 2 ** -8 * gelu.abs() + 1e-6).all()
+    assert ((d2[:, 2560:] - dgelu).abs() <= 2 ** -8 * dgelu.abs() + 1e-6).all()
 
 
 def test_silu_concat_pool_colsum(dev):
