@@ -265,6 +265,8 @@ int otamd_layernorm_param_grad(const void* x, long long ldx, const void* dy, lon
 int otamd_layernorm_defer_begin(hipStream_t stream, void* arena, long long bytes);
 int otamd_layernorm_defer_flush(hipStream_t stream);
 int otamd_layernorm_defer_end(hipStream_t stream);
+/* the same with the pending reduces launched on `launch`, which the caller has ordered after `stream` */
+int otamd_layernorm_defer_end_on(hipStream_t stream, hipStream_t launch);
 /* out[0] LayerNorms deferred, out[1] grouped launches (totals since load), out[2] pending on `stream` */
 int otamd_layernorm_defer_stats(hipStream_t stream, long long* out);
 

@@ -105,6 +105,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_layernorm_defer_begin": [VP, VP, LL],
     "otamd_layernorm_defer_flush": [VP],
     "otamd_layernorm_defer_end": [VP],
+    "otamd_layernorm_defer_end_on": [VP, VP],
     "otamd_layernorm_defer_stats": [VP, VP],
     "otamd_layernorm_bwd_res": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP],
     "otamd_layernorm_bwd_fused": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],

@@ -1047,16 +1047,18 @@ OTAMD_API int otamd_layernorm_defer_flush(hipStream_t stream) {
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
-// flush and leave defer mode
-OTAMD_API int otamd_layernorm_defer_end(hipStream_t stream) {
+// flush and leave defer mode; the pending reduces go out on `launch` (the caller orders it after `stream`'s
+// parameter passes: the two-stream step flushes on the weight-gradient stream, whose join ends the backward)
+OTAMD_API int otamd_layernorm_defer_end_on(hipStream_t stream, hipStream_t launch) {
   std::lock_guard<std::mutex> lk(g_ln_defer_mu);
   auto it = g_ln_defer.find(stream);
   if (it == g_ln_defer.end()) return OTAMD_OK;
-  ln_defer_flush_locked(it->second, stream);
+  ln_defer_flush_locked(it->second, launch);
   g_ln_defer.erase(it);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }
+OTAMD_API int otamd_layernorm_defer_end(hipStream_t stream) { return otamd_layernorm_defer_end_on(stream, stream); }
 // out[0] = LayerNorms whose parameter reduce went out deferred, out[1] = grouped launches, out[2] = pending on stream
 OTAMD_API int otamd_layernorm_defer_stats(hipStream_t stream, long long* out) {
   if (!out) return OTAMD_EINVAL;

@@ -109,8 +109,11 @@ def ln_defer_flush(stream) -> None:
     check(lib().otamd_layernorm_defer_flush(C.c_void_p(stream.cuda_stream)), "otamd_layernorm_defer_flush")
 
 
-def ln_defer_end(stream) -> None:
-    check(lib().otamd_layernorm_defer_end(C.c_void_p(stream.cuda_stream)), "otamd_layernorm_defer_end")
+def ln_defer_end(stream, launch=None) -> None:
+    """flush and leave defer mode; launch: the stream the pending reduces go out on (ordered after `stream` by the
+    caller; default `stream`)"""
+    check(lib().otamd_layernorm_defer_end_on(C.c_void_p(stream.cuda_stream),
+                                             C.c_void_p((launch or stream).cuda_stream)), "otamd_layernorm_defer_end_on")
 
 
 def ln_defer_stats(stream) -> tuple:

@@ -150,10 +150,18 @@ def defer_flush():
 
 
 def defer_end():
+    side = side_stream()
     if _LN_STREAM:
         from .. import kernels as K
-        K.ln_defer_end(_LN_STREAM.pop())
-    side = side_stream()
+        main = _LN_STREAM.pop()
+        if side is not None:
+            # the last LayerNorm reduces go out on the side stream after everything queued on the main stream, so a
+            # captured step (trainer/step_graph.py) still ends in one sink: the side chain's last node, which the
+            # join hands back to the main stream
+            side.wait_stream(main)
+            K.ln_defer_end(main, launch=side)
+        else:
+            K.ln_defer_end(main)
     if side is not None and _DEFER:
         from .. import kernels as K
         K.defer_reduces_end(side)

@@ -9,6 +9,8 @@
   weight-gradient branch has (the join into store.finish_backward is an edge), and every fork of the side
   branch hangs off the main chain.
 """
+import re
+
 import pytest
 import torch
 
@@ -95,7 +97,14 @@ def test_step_graph_single_sink(dev, tmp_path, monkeypatch):
         tr.train_step(batch)                        # the capture
     torch.cuda.synchronize()
     s = structure(str(dot))
-    assert s["nodes"] > 100 and len(s["roots"]) == 1 and len(s["leaves"]) == 1, s
+    raw = dot.read_text(errors="replace")
+
+    def kernel_of(n):   # the node's kernel symbol from its DOT record (for the failure message)
+        i = raw.find(f'"{n}"[')
+        m = re.search(r"ID \| \d+ \| (\S+)", raw[i:i + 600]) if i >= 0 else None
+        return m.group(1)[:80] if m else "?"
+    assert s["nodes"] > 100 and len(s["roots"]) == 1 and len(s["leaves"]) == 1, \
+        (s["nodes"], [(n, kernel_of(n)) for n in s["roots"]], [(n, kernel_of(n)) for n in s["leaves"]])
     # every side region forks the side chain off the main chain (a node with two successors); a region whose
     # fork was missing would start a second root instead
     assert s["forks"] >= 0.5 * chk.regions, (s["forks"], chk.regions)

@@ -73,8 +73,12 @@ def main():
     s = structure(a.out)
     print(f"{a.out}: {s['nodes']} nodes, {s['edges']} edges, {len(s['roots'])} roots, {len(s['leaves'])} leaves, "
           f"{s['joins']} joins, {s['forks']} forks")
+    raw = open(a.out, errors="replace").read().splitlines()
     for n in s["leaves"][:10]:
         print("  leaf", n, s["labels"][n][:160])
+        for line in raw:   # the node's own DOT lines (kernel name / node type) and its incoming edges
+            if re.search(r'\b%s\b' % n, line):
+                print("     ", line.strip()[:300])
     return 0
 
 

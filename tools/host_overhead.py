@@ -1,5 +1,6 @@
 """Host issue time vs GPU time of the SDXL train step (1024^2, b=4): for each step, the time the
-Python host needs to enqueue the whole step (no sync) and the step's wall time to completion."""
+Python host needs to enqueue the whole step (no sync) and the step's wall time to completion.
+HO_LORA=<rank>: the LoRA step (C4: r32); HO_PROFILE=1: cProfile of one step."""
 import os
 import sys
 import time
@@ -15,6 +16,8 @@ from onetrainer_amd.util.config.TrainConfig import TrainConfig  # noqa: E402
 dev = torch.device("cuda:0")
 cfg = TrainConfig.default_values()
 cfg.batch_size = int(os.environ.get("HO_BATCH", "4"))
+if int(os.environ.get("HO_LORA", "0")):
+    cfg.training_method, cfg.lora_rank = "LORA", int(os.environ["HO_LORA"])
 model = create.create_model(cfg, dev, seed=0)
 tr = GenericTrainer(cfg, model=model)
 tr.start()
