@@ -1254,11 +1254,18 @@ static int ln_param_grads(const void* x, long long ldx, const void* dy, long lon
                           const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32,
                           int param_acc, float* part, hipStream_t stream) {
   {
-    // ~256 blocks (one per CU) of >= 32 rows (4 per wave, one unrolled batch), at most 512 slabs (the
-    // part buffer holds 1024 x 2C floats): few slabs keep the second (reduce) pass short -- with
-    // 16-row slabs both passes were latency-bound (~11 us + ~8.5 us per LayerNorm at 4096 x 1280)
+    // ~512 blocks of >= 32 rows (4 per wave, one unrolled batch), at most 512 slabs (the part buffer holds
+    // 1024 x 2C floats): few slabs keep the second (reduce) pass short -- with 16-row slabs both passes were
+    // latency-bound (~11 us + ~8.5 us per LayerNorm at 4096 x 1280)
+    // workgroups per parameter pass: 512 (two per CU) measured -0.11 ms per SDXL step against 256 once the slab
+    // reduce went out grouped (profiles/r5_ln_param_blocks_ab.txt); OTAMD_LN_PARAM_BLOCKS overrides (A/B)
+    static const int target = [] {
+      const char* e = getenv("OTAMD_LN_PARAM_BLOCKS");
+      const int v = e ? atoi(e) : 0;
+      return v > 0 ? v : 512;
+    }();
     const int cb = (C / 8 + 63) / 64;
-    int slabs = (256 + cb - 1) / cb;
+    int slabs = (target + cb - 1) / cb;
     slabs = min(slabs, max(1, rows / 32));
     slabs = min(slabs, 512);
     const int rps = (rows + slabs - 1) / slabs;
