@@ -60,7 +60,6 @@ typedef struct GemmArgs {
      GEMM slabs (splits * M floats) and the split-K reduce folds them */
   void* colsum; int colsum_f32; int colsum_acc;
   float* colsum_slab;
-  int* tile_sem;   /* launcher-internal (the in-launch split-K combine's ticket counters): callers leave it 0 */
 } GemmArgs;
 
 typedef struct AttnArgs {
@@ -242,14 +241,6 @@ int otamd_layernorm_bwd_res(const void* x, long long ldx, const void* dy, long l
     long long ldres, void* dx, long long lddx, int rows, int C, const void* gamma, const float* mean,
     const float* rstd, hipStream_t stream);
 
-/* replaces: the same backward (+ the residual gradient dres, nullable; or + dx when accumulate) AND
-   dgamma / dbeta in one pass over x and dy (otamd_layernorm_bwd_res + otamd_layernorm_param_grad read both twice);
-   part: float scratch >= 1024 * 2 * C.  OTAMD_EUNSUPPORTED (nothing launched) for widths without a row-group form. */
-int otamd_layernorm_bwd_fused(const void* x, long long ldx, const void* dy, long long lddy, const void* dres,
-                              long long ldres, void* dx, long long lddx, int rows, int C, const void* gamma,
-                              const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32,
-                              int param_acc, float* part, int accumulate, hipStream_t stream);
-
 /* replaces: the LayerNorm weight / bias gradient half of the same autograd node (dgamma = sum dy xhat,
    dbeta = sum dy), issued separately so it can run on the weight-gradient side stream */
 int otamd_layernorm_param_grad(const void* x, long long ldx, const void* dy, long long lddy, int rows, int C,
@@ -351,19 +342,6 @@ int otamd_gemm_defer_end(hipStream_t stream);
 int otamd_gemm_defer_pending(hipStream_t stream);
 int otamd_gemm_defer_stats(long long* out);
 
-/* replaces: nothing (engine control): the in-launch split-K combine.  A split-K GEMM on the v2 tiles without fused
-   column sums whose per-tile slab traffic (splits * tile bytes in fp32) is at most this many bytes sums its slabs
-   in the workgroup that finishes a tile last (ticket counter, agent-scope release / acquire), bit-identical to
-   the reduce launch it replaces.  Default OTAMD_GEMM_FIXUP_KB (0: always a reduce launch; measured slower in the step), -1 = back to
-   the default.  Returns the previous limit. */
-long long otamd_gemm_set_fixup_limit(long long bytes);   /* out[0] deferred GEMMs, out[1] grouped launches, since load */
-
-/* replaces: nothing (engine control): the K-loop schedule of the v2 GEMM tiles, 0 = whole 64-deep K-tile DMA per
-   stage (gemm2_kernel.h), 1 = half-K DMA units with two units in flight across every barrier (gemm2h_kernel.h),
-   2 = half-K units for the MN-mode-A (weight-gradient) GEMMs only; any other value only queries.  Returns the
-   previous schedule.  Default: OTAMD_GEMM_HK, else 0. */
-int otamd_gemm_set_schedule(int hk);
-
 /* replaces: nothing in the reference (it has no DP): the on-chip footprint of one gradient bucket's RCCL ring
    all-reduce, emulated on one GPU for the step-slowdown measurement of DESIGN.md §6 (trainer/ddp.py
    OTAMD_DP_EMULATE): `blocks` workgroups copy `bytes` from src to dst (each wrapping over its size), paced to take
@@ -428,7 +406,14 @@ int otamd_adamw_bf16_range(void* p, const void* g, void* m, void* v, long long b
 int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long long n, const AdamwGroup* groups, int
     n_groups, const float* clip_coef, hipStream_t stream);
 
+/* replaces: same, fp32 master weights of a full fine-tune (weight_dtype FLOAT_32, TrainConfig.py:782, under a bf16
+   autocast, dtype_util.py:28-49): p32 / m32 / v32 fp32, g16 the bf16 gradient store, w16 the bf16 working copy the
+   GEMMs read, rewritten as rne(p32) (autocast's cast); elements [begin, end), multiples of 8 */
+int otamd_adamw_master_range(void* p32, const void* g16, void* m32, void* v32, void* w16, long long begin,
+    long long end, const AdamwGroup* groups, int n_groups, const float* clip_coef, hipStream_t stream);
+
 /* replaces: nn.utils.clip_grad_norm_(parameters, clip_grad_norm) (modules/trainer/GenericTrainer.py:712-713);
+   grad_dtype 0 bf16, 1 fp32, 2 bf16 storage of fp32-master gradients (norms and coefficient in fp32); 
    chunk_sq: double[n_chunks] scratch (one slot per chunk, summed per tensor in chunk order: deterministic) */
 int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void* chunks, int n_chunks, double* chunk_sq,
     double* tensor_sq, int n_tensors, float max_norm, float* out, hipStream_t stream);

@@ -34,8 +34,7 @@ class GemmArgs(C.Structure):
                 ("K1", C.c_int), ("K2", C.c_int),
                 ("batch", C.c_int), ("bdiv", C.c_int), ("sa0", C.c_longlong), ("sa1", C.c_longlong),
                 ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong),
-                ("colsum", C.c_void_p), ("colsum_f32", C.c_int), ("colsum_acc", C.c_int), ("colsum_slab", C.c_void_p),
-                ("tile_sem", C.c_void_p)]
+                ("colsum", C.c_void_p), ("colsum_f32", C.c_int), ("colsum_acc", C.c_int), ("colsum_slab", C.c_void_p)]
 
 
 class AdamwGroup(C.Structure):
@@ -90,6 +89,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_adamw_bf16": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_bf16_range": [VP, VP, VP, VP, LL, LL, C.POINTER(AdamwGroup), I, VP, I, C.c_ulonglong, VP],
     "otamd_adamw_f32": [VP, VP, VP, VP, LL, C.POINTER(AdamwGroup), I, VP, VP],
+    "otamd_adamw_master_range": [VP, VP, VP, VP, VP, LL, LL, C.POINTER(AdamwGroup), I, VP, VP],
     "otamd_grad_clip_coef": [VP, I, VP, I, VP, VP, I, F, VP, VP],
     "otamd_grad_sqnorm_chunks": [VP, I, VP, I, I, VP, VP],
     "otamd_grad_clip_finalize": [VP, I, VP, VP, I, F, I, VP, VP],
@@ -108,7 +108,6 @@ SIGNATURES: dict[str, list] = {
     "otamd_layernorm_defer_end_on": [VP, VP],
     "otamd_layernorm_defer_stats": [VP, VP],
     "otamd_layernorm_bwd_res": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP],
-    "otamd_layernorm_bwd_fused": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, VP, VP, VP, VP, I, I, VP, I, VP],
     # attention.hip
     "otamd_attn_args_size": [],
     "otamd_attn_fwd": [C.POINTER(AttnArgs), VP],
@@ -140,13 +139,11 @@ SIGNATURES: dict[str, list] = {
     "otamd_timestep_embedding": [VP, I, I, VP, LL, VP],
     "otamd_add": [VP, VP, VP, LL, VP],
     "otamd_dp_emulate": [VP, LL, VP, LL, LL, I, LL, VP],
-    "otamd_gemm_set_schedule": [I],
     "otamd_gemm_defer_begin": [VP, VP, LL, VP, LL],
     "otamd_gemm_defer_flush": [VP],
     "otamd_gemm_defer_end": [VP],
     "otamd_gemm_defer_pending": [VP],
     "otamd_gemm_defer_stats": [VP],
-    "otamd_gemm_set_fixup_limit": [LL],
     "otamd_image_to_nhwc": [VP, I, I, I, I, F, F, VP, I, VP],
     # flux.hip
     "otamd_adaln_fwd": [VP, LL, VP, LL, I, I, F, VP, LL, I, I, I, VP, VP, VP],
@@ -192,7 +189,7 @@ def lib():
                 continue
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_slab_bytes", "_plan", "_part_floats", "_fixup_limit")) else C.c_int
+            fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_slab_bytes", "_plan", "_part_floats")) else C.c_int
         _lib = L
     return _lib
 

@@ -210,6 +210,20 @@ __global__ void __launch_bounds__(1024) adamw_bf16_lut_kernel(bf16_t* __restrict
   }
 }
 
+// one element of the fp32 path: every torch op of step_adamw_parameter on fp32 tensors rounds to fp32
+// (p.mul_, exp_avg.lerp_ (fma), exp_avg_sq.mul_().addcmul_ (fma), sqrt()/bc2_sqrt .add_(eps), p.addcdiv_);
+// the clipped gradient is _foreach_mul_(grads, clip_coef) in fp32.  Restated in oracle/adamw.py adamw_step_f32.
+__device__ __forceinline__ void adamw_elem_f32(float& p, float g, float& m, float& v, const AdamwGroup& G, float coef,
+                                               bool clip) {
+  if (clip) g = g * coef;
+  p = p * G.wd_factor;
+  m = fmaf(G.one_minus_beta1, g - m, m);
+  v = v * G.beta2;
+  v = fmaf(G.one_minus_beta2 * g, g, v);
+  const float d = sqrtf(v) / G.bc2_sqrt + G.eps;
+  p = p + (G.neg_step_size * m) / d;
+}
+
 // fp32 store (LoRA weights are fp32 by default, TrainConfig.py:959): plain fp32 torch ops
 __global__ void __launch_bounds__(256) adamw_f32_kernel(float* __restrict__ P, const float* __restrict__ Gr,
                                                         float* __restrict__ M, float* __restrict__ V, long long n4,
@@ -227,18 +241,44 @@ __global__ void __launch_bounds__(256) adamw_f32_kernel(float* __restrict__ P, c
     float4 vv = reinterpret_cast<const float4*>(V)[i];
     float* p = &pv.x; float* g = &gv.x; float* m = &mv.x; float* v = &vv.x;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gg = clip ? g[j] * coef : g[j];
-      p[j] = p[j] * G.wd_factor;
-      m[j] = fmaf(G.one_minus_beta1, gg - m[j], m[j]);
-      v[j] = v[j] * G.beta2;
-      v[j] = fmaf(G.one_minus_beta2 * gg, gg, v[j]);
-      float d = sqrtf(v[j]) / G.bc2_sqrt + G.eps;
-      p[j] = p[j] + (G.neg_step_size * m[j]) / d;
-    }
+    for (int j = 0; j < 4; ++j) adamw_elem_f32(p[j], g[j], m[j], v[j], G, coef, clip);
     reinterpret_cast<float4*>(P)[i] = pv;
     reinterpret_cast<float4*>(M)[i] = mv;
     reinterpret_cast<float4*>(V)[i] = vv;
+  }
+}
+
+// fp32 master weights of a full fine-tune (the reference's default weight_dtype FLOAT_32, TrainConfig.py:782, with
+// a bf16 train_dtype: autocast runs every GEMM on a bf16 cast of the fp32 weight, and its weight gradient is the bf16
+// GEMM result cast back to fp32).  The kernels read a bf16 working copy and write bf16 gradients, so per element:
+// read g (bf16) and p, m, v (fp32), the fp32 step above, write p, m, v and the working copy rne(p) -- the
+// round-to-nearest cast autocast applies at the next forward.  28 B per element.
+struct __align__(16) f8 { float4 a, b; };
+__global__ void __launch_bounds__(256) adamw_master_kernel(float* __restrict__ P, const bf16_t* __restrict__ Gr,
+                                                           float* __restrict__ M, float* __restrict__ V,
+                                                           bf16_t* __restrict__ W, long long v0, long long n8,
+                                                           AdamwGroups groups, const float* __restrict__ clip_coef) {
+  const bool clip = clip_coef != nullptr;
+  const float coef = clip ? clip_coef[0] : 1.f;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = v0 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const long long e0 = i * 8;
+    const int gi = find_group(groups, e0);
+    const AdamwGroup& G = groups.g[gi];
+    if (e0 >= G.end) continue;
+    const bf8 gv = reinterpret_cast<const bf8*>(Gr)[i];
+    f8 pv = reinterpret_cast<const f8*>(P)[i];
+    f8 mv = reinterpret_cast<const f8*>(M)[i];
+    f8 vv = reinterpret_cast<const f8*>(V)[i];
+    float g[8];
+    unpack8(gv, g);
+    float* p = &pv.a.x; float* m = &mv.a.x; float* v = &vv.a.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adamw_elem_f32(p[j], g[j], m[j], v[j], G, coef, clip);
+    reinterpret_cast<f8*>(P)[i] = pv;
+    reinterpret_cast<f8*>(M)[i] = mv;
+    reinterpret_cast<f8*>(V)[i] = vv;
+    reinterpret_cast<bf8*>(W)[i] = pack8(p);
   }
 }
 
@@ -413,7 +453,30 @@ OTAMD_API int otamd_adamw_f32(void* p, const void* g, void* m, void* v, long lon
   return OTAMD_OK;
 }
 
-// grads: flat store (bf16 if grad_dtype==0 else f32); chunks: device table of n_chunks NormChunk;
+// p32 / m32 / v32: fp32 flat buffers; g16: the bf16 gradient store; w16: the bf16 working copy the kernels read;
+// [begin, end): element range (multiples of 8)
+OTAMD_API int otamd_adamw_master_range(void* p32, const void* g16, void* m32, void* v32, void* w16, long long begin,
+                                       long long end, const AdamwGroup* groups, int n_groups, const float* clip_coef,
+                                       hipStream_t stream) {
+  if (!p32 || !g16 || !m32 || !v32 || !w16 || begin < 0 || end < begin || (begin % 8) != 0 || (end % 8) != 0 ||
+      n_groups < 1 || n_groups > ADAMW_MAX_GROUPS)
+    return OTAMD_EINVAL;
+  if (((uintptr_t)p32 | (uintptr_t)g16 | (uintptr_t)m32 | (uintptr_t)v32 | (uintptr_t)w16) & 15) return OTAMD_EINVAL;
+  if (end == begin) return OTAMD_OK;
+  AdamwGroups G = {};
+  for (int i = 0; i < n_groups; ++i) G.g[i] = groups[i];
+  G.n = n_groups;
+  const long long v0 = begin / 8, v1 = end / 8;
+  const int blocks = (int)std::max(1LL, std::min<long long>((v1 - v0 + 255) / 256, 256 * 16));
+  adamw_master_kernel<<<blocks, 256, 0, stream>>>((float*)p32, (const bf16_t*)g16, (float*)m32, (float*)v32,
+                                                  (bf16_t*)w16, v0, v1, G, clip_coef);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
+// grads: flat store, grad_dtype 0 = bf16, 1 = f32, 2 = bf16 storage of an fp32-master network's gradients (the
+// reference holds them as fp32 tensors: clip_grad_norm_ forms the norms and the coefficient in fp32);
+// chunks: device table of n_chunks NormChunk;
 OTAMD_API int otamd_grad_clip_finalize(const void* chunks, int n_chunks, const double* chunk_sq, double* tensor_sq,
                                        int n_tensors, float max_norm, int grad_dtype, float* out, hipStream_t stream);
 
@@ -423,8 +486,9 @@ OTAMD_API int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void
                                    double* tensor_sq, int n_tensors, float max_norm, float* out, hipStream_t stream) {
   if (!grads || !chunks || !tensor_sq || !out || n_chunks < 0 || n_tensors < 1 || (n_chunks > 0 && !chunk_sq))
     return OTAMD_EINVAL;
+  if (grad_dtype < 0 || grad_dtype > 2) return OTAMD_EINVAL;
   if (n_chunks > 0) {
-    if (grad_dtype == 0)
+    if (grad_dtype != 1)
       grad_sqnorm_kernel<bf16_t><<<n_chunks, 256, 0, stream>>>((const bf16_t*)grads, (const NormChunk*)chunks, chunk_sq);
     else
       grad_sqnorm_kernel<float><<<n_chunks, 256, 0, stream>>>((const float*)grads, (const NormChunk*)chunks, chunk_sq);
@@ -438,10 +502,11 @@ OTAMD_API int otamd_grad_clip_coef(const void* grads, int grad_dtype, const void
 // weight-gradient stream beside the dgrad chain ...
 OTAMD_API int otamd_grad_sqnorm_chunks(const void* grads, int grad_dtype, const void* chunks, int c_begin, int c_end,
                                        double* chunk_sq, hipStream_t stream) {
-  if (!grads || !chunks || !chunk_sq || c_begin < 0 || c_end < c_begin) return OTAMD_EINVAL;
+  if (!grads || !chunks || !chunk_sq || c_begin < 0 || c_end < c_begin || grad_dtype < 0 || grad_dtype > 2)
+    return OTAMD_EINVAL;
   if (c_end == c_begin) return OTAMD_OK;
   const NormChunk* c = (const NormChunk*)chunks + c_begin;
-  if (grad_dtype == 0)
+  if (grad_dtype != 1)
     grad_sqnorm_kernel<bf16_t><<<c_end - c_begin, 256, 0, stream>>>((const bf16_t*)grads, c, chunk_sq + c_begin);
   else
     grad_sqnorm_kernel<float><<<c_end - c_begin, 256, 0, stream>>>((const float*)grads, c, chunk_sq + c_begin);
@@ -453,7 +518,9 @@ OTAMD_API int otamd_grad_sqnorm_chunks(const void* grads, int grad_dtype, const 
 // dtypes (as otamd_grad_clip_coef)
 OTAMD_API int otamd_grad_clip_finalize(const void* chunks, int n_chunks, const double* chunk_sq, double* tensor_sq,
                                        int n_tensors, float max_norm, int grad_dtype, float* out, hipStream_t stream) {
-  if (!chunks || !tensor_sq || !out || n_tensors < 1 || n_chunks < 0 || (n_chunks > 0 && !chunk_sq)) return OTAMD_EINVAL;
+  if (!chunks || !tensor_sq || !out || n_tensors < 1 || n_chunks < 0 || (n_chunks > 0 && !chunk_sq) || grad_dtype < 0 ||
+      grad_dtype > 2)
+    return OTAMD_EINVAL;
   if (hipMemsetAsync(tensor_sq, 0, sizeof(double) * n_tensors, stream) != hipSuccess) return OTAMD_ELAUNCH;
   if (n_chunks > 0) {
     tensor_sq_kernel<<<(n_chunks + 255) / 256, 256, 0, stream>>>((const NormChunk*)chunks, n_chunks, chunk_sq, tensor_sq);

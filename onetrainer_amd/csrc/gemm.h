@@ -45,9 +45,6 @@ struct GemmArgs {
   // split-K reduce.  v2 tiles only; tile-column 0 workgroups accumulate them from the LDS image of A.
   void* colsum; int colsum_f32; int colsum_acc;
   float* colsum_slab;
-  // in-launch split-K combine (set by the launcher, never by callers): one ticket counter per tile, zero between
-  // launches; the workgroup drawing a tile's last ticket sums its slabs (splitk_fixup).  nullptr: a reduce launch.
-  int* tile_sem;
 };
 
 __device__ __forceinline__ void gemm_batch_offset(GemmArgs& a) {
@@ -268,36 +265,4 @@ __device__ __forceinline__ void splitk_combine(const GemmArgs& args, unsigned m,
   }
 }
 
-// In-launch split-K combine (cdna_hip_programming.md, "In-launch split-K reduction", plain-store form): every
-// K-slice workgroup of a tile has stored its fp32 slab; each drains its stores, lane 0 releases at agent scope and
-// draws a ticket; the workgroup drawing the last one acquires and sums the tile's slabs in split order with the
-// epilogue (splitk_combine: the numbers splitk_reduce_kernel produces), then resets the counter for the next
-// launch.  Correct for any placement of a tile's slices over the XCDs.  `flag`: a word of the kernel's one LDS
-// array (the ring is dead once every wave is past the K loop: the first barrier here).
-template <int BM, int BN>
-__device__ __forceinline__ void splitk_fixup(const GemmArgs& args, int m0, int n0, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(args.tile_sem + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == (int)gridDim.z - 1;
-    if (last) {
-      __hip_atomic_store(args.tile_sem + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  const int splits = gridDim.z;
-  constexpr int CV = BN / 4;
-  for (int e = threadIdx.x; e < BM * CV; e += blockDim.x) {
-    const int r = e / CV, c = (e - r * CV) * 4;
-    const int m = m0 + r, n = n0 + c;
-    if (m < args.M && n < args.N) splitk_combine<4>(args, m, n, splits);
-  }
-}
 

@@ -488,54 +488,6 @@ OTAMD_API int otamd_gemm_defer_pending(hipStream_t stream) {
   return it == g_defer.end() ? 0 : it->second.batch.n;
 }
 
-// ---- in-launch split-K combine (splitk_fixup, gemm.h) -------------------------------------------------------------
-// Per-stream ticket counters, zeroed once when allocated and left zero by every launch (the last arriver resets its
-// tile's word).  A split-K GEMM of the v2 tiles without fused column sums whose per-tile slab traffic
-// (splits * BM * BN * 4 bytes) is at most OTAMD_GEMM_FIXUP_KB (default 0 = off: measured slower) combines in-launch instead of
-// launching splitk_reduce_kernel.  Never allocated under stream capture (that launch keeps the reduce launch).
-constexpr int kSemTiles = 1 << 16;
-static std::mutex g_sem_mu;
-static std::unordered_map<hipStream_t, int*> g_sem;
-
-static long long fixup_limit() {
-  static const long long kb = [] {
-    const char* e = getenv("OTAMD_GEMM_FIXUP_KB");
-    return e ? atoll(e) : 0LL;
-  }();
-  return kb << 10;
-}
-static std::atomic<long long> g_fixup_override{-1};
-// A/B: force the in-launch combine's per-tile byte limit (bytes; -1 = OTAMD_GEMM_FIXUP_KB); returns the previous
-OTAMD_API long long otamd_gemm_set_fixup_limit(long long bytes) {
-  const long long prev = g_fixup_override.exchange(bytes);
-  return prev < 0 ? fixup_limit() : prev;
-}
-
-static int* tile_sems(hipStream_t stream) {
-  std::lock_guard<std::mutex> lk(g_sem_mu);
-  auto it = g_sem.find(stream);
-  if (it != g_sem.end()) return it->second;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  int* p = nullptr;
-  if (hipMalloc(&p, kSemTiles * sizeof(int)) != hipSuccess) return nullptr;
-  if (hipMemset(p, 0, kSemTiles * sizeof(int)) != hipSuccess) { (void)hipFree(p); return nullptr; }
-  g_sem[stream] = p;
-  return p;
-}
-
-static int* fixup_sems(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
-  static const int geo[11][2] = {{256, 256}, {256, 128}, {128, 256}, {256, 256}, {128, 128}, {128, 64},
-                                 {64, 128},  {128, 160}, {256, 160}, {128, 64},  {64, 128}};
-  if (splits <= 1 || tile < 0 || tile > 10 || a.colsum || a.batch > 1) return nullptr;
-  const long long ov = g_fixup_override.load(std::memory_order_relaxed);
-  const long long lim = ov >= 0 ? ov : fixup_limit();
-  const int bm = geo[tile][0], bn = geo[tile][1];
-  if ((long long)splits * bm * bn * 4 > lim) return nullptr;
-  if ((long long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) > kSemTiles) return nullptr;
-  return tile_sems(stream);
-}
-
 typedef void (*gemm_fn)(GemmArgs);
 
 static gemm_fn pick(int am, int bm) {
@@ -694,7 +646,6 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
                      hipStream_t stream) {
   if (!in) return OTAMD_EINVAL;
   GemmArgs a = *in;
-  a.tile_sem = nullptr;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
   const bool v2_only = a.bmode == OPM_CONV_WT || a.A2 != nullptr;
   if (a.A2) {   // second K segment (LoRA fusion): forms and alignment the v2 kernels support
@@ -751,12 +702,9 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   if (a.colsum && (tile < 0 || tile == 3)) tile = 0;   // the fused column sums live in the 8-wave v2 kernels
   if (v2_only && tile < 0) return OTAMD_EUNSUPPORTED;
   int rc = OTAMD_EUNSUPPORTED;
-  if (!deferred) a.tile_sem = fixup_sems(a, tile, splits, stream);
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
-  const bool combined = rc == OTAMD_OK && a.tile_sem != nullptr;   // the v2 kernel combined its splits in-launch
   if (rc != OTAMD_OK) {
-    a.tile_sem = nullptr;
     if (!fn || a.A2 || a.colsum) return rc;   // v1 has no conv-weight B, no second K segment, no column sums
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid(tiles, a.batch > 1 ? a.batch : 1, splits);
@@ -765,7 +713,7 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   }
   if (deferred) {
     defer_record(a, splits, stream);
-  } else if (splits > 1 && !combined) {
+  } else if (splits > 1) {
     // 8-wide needs 16-byte aligned rows of C (bf16: ldc % 8, fp32 handled element-wise)
     const bool v8 = (a.N % 8) == 0 && (a.ldc % 8) == 0 && ((uintptr_t)a.C & 15) == 0;
     const long long nv = (long long)a.M * a.N / (v8 ? 8 : 4);

@@ -2,7 +2,6 @@
 // gemm2_tiles_*.hip, one translation unit per tile family so they compile in parallel).
 #include "gemm2_kernel.h"
 
-#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <unordered_set>
@@ -11,8 +10,6 @@ gemm2_fn gemm2_pick_a(int tile, int am, int bm, bool seg2, bool cs);   // 0, 3  
 gemm2_fn gemm2_pick_b(int tile, int am, int bm, bool seg2, bool cs);   // 1, 2   256x128, 128x256
 gemm2_fn gemm2_pick_c(int tile, int am, int bm, bool seg2, bool cs);   // 4, 5, 6, 9, 10  128x128, 128x64, 64x128
 gemm2_fn gemm2_pick_d(int tile, int am, int bm, bool seg2, bool cs);   // 7, 8   x160
-gemm2_fn gemm2h_pick_a(int tile, int am, int bm, bool cs);   // half-K DMA units (gemm2h_kernel.h): 0, 1, 2
-gemm2_fn gemm2h_pick_b(int tile, int am, int bm, bool cs);   // 4, 7, 8
 
 // byte extent an operand's gathers may touch (the DMA descriptor's range)
 static long long operand_bytes(int mode, const bf16_t* p, long long ld, int MN, int K, const ConvGeom& g) {
@@ -20,29 +17,6 @@ static long long operand_bytes(int mode, const bf16_t* p, long long ld, int MN, 
   if (mode == OPM_K) return ((long long)(MN - 1) * ld + K) * 2;
   if (mode == OPM_MN || mode == OPM_CONV_WT) return ((long long)(K - 1) * ld + MN) * 2;
   return ((long long)g.N * g.SH * g.SW - 1) * g.ld * 2 + (long long)g.SC * 2;
-}
-
-static std::atomic<int> g_hk{-1};
-static int gemm_hk_schedule() {
-  int v = g_hk.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("OTAMD_GEMM_HK");
-    v = e && (e[0] == '0' || e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
-    g_hk.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-// select the K-loop schedule of the v2 tiles: 0 = whole K-tile DMA everywhere (gemm2_kernel.h); 1 = half-K DMA
-// units everywhere they exist (gemm2h_kernel.h); 2 = half-K units where they measured faster alone, the
-// MN-mode-A GEMMs (weight gradients: 10240x1280x4096 +6-10 %, 1280x1280x4096 +14-18 %, 1280x5120x4096 +9 %; the K-mode
-// forms lost 4-23 %: their half images have 64-byte rows, half-line source segments; profiles/r5_gemm_hk_ab.jsonl).
-// In the SDXL step (tools/gpu_ab_hk.sh, profiles/r5_gemm_hk_step_ab.txt) 2 ran 131.9 -> 132.1 ms (the weight-gradient
-// stream is off the critical path) and 1 137.3 ms, so 0 stays the default.
-// Returns the previous schedule (A/B in one process: tools/gemm_hk_ab.py).
-OTAMD_API int otamd_gemm_set_schedule(int hk) {
-  const int prev = gemm_hk_schedule();
-  if (hk >= 0 && hk <= 2) g_hk.store(hk, std::memory_order_relaxed);
-  return prev;
 }
 
 // launched by otamd_gemm (gemm.hip) when the v2 tile is selected; returns OTAMD_EUNSUPPORTED
@@ -67,17 +41,7 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   // OTAMD_SKINNY_NS4=1: tiles 5 / 6 run on the 4-deep ring (tiles 9 / 10) when they have no second K segment
   static const bool skinny4 = [] { const char* e = getenv("OTAMD_SKINNY_NS4"); return e && e[0] == '1'; }();
   if (skinny4 && (tile == 5 || tile == 6) && !seg2) tile += 4;
-  // the half-K-unit schedule (gemm2h_kernel.h) for the plain single-segment instances: OTAMD_GEMM_HK=1 or
-  // otamd_gemm_set_schedule(1)
-  const int hk = gemm_hk_schedule();
-  // auto (2): MN-mode A without the column sums, or with them on the 128-row tiles (the 256-row tiles keep their
-  // colsum partials in LDS, read-modified per half image: 10240x1280x4096 -9 %, 640x640x16384 -10 %)
-  const bool hk_auto = a.amode == OPM_MN && (!cs || tile == 2 || tile == 4 || tile == 7);
-  if (!seg2 && (hk == 1 || (hk == 2 && hk_auto))) {
-    if (tile == 0 || tile == 1 || tile == 2) fn = gemm2h_pick_a(tile, a.amode, a.bmode, cs);
-    else if (tile == 4 || tile == 7 || tile == 8) fn = gemm2h_pick_b(tile, a.amode, a.bmode, cs);
-  }
-  if (!fn) switch (tile) {
+  switch (tile) {
     case 0: case 3: fn = gemm2_pick_a(tile, a.amode, a.bmode, seg2, cs); break;
     case 1: case 2: fn = gemm2_pick_b(tile, a.amode, a.bmode, seg2, cs); break;
     case 4: case 5: case 6: case 9: case 10: fn = gemm2_pick_c(tile, a.amode, a.bmode, seg2, cs); break;

@@ -579,7 +579,6 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
         }
       }
     }
-    if (use_slab && args.tile_sem) splitk_fixup<BM, BN>(args, m0, n0, reinterpret_cast<int*>(smem));
     return;
   }
 #pragma unroll

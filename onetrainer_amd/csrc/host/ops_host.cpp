@@ -392,30 +392,6 @@ py::object layernorm_bwd_res(const Tensor& x, const Tensor& dy, const Tensor& dr
   return py::cast(dx);
 }
 
-// dx = LayerNorm-backward(dy) (+ dres) and dgamma / dbeta in one pass; None when the width has no fused form
-py::object layernorm_bwd_fused(const Tensor& x, const Tensor& dy, const optional<Tensor>& dres, const Tensor& gamma,
-                               const Tensor& mean, const Tensor& rstd, const Tensor& dgamma, const Tensor& dbeta,
-                               bool param_acc, int64_t stream) {
-  const Rows r = rows2d(x), rd = rows2d(dy);
-  req(dgamma.scalar_type() == dbeta.scalar_type() && (is_bf16(dgamma) || is_f32(dgamma)),
-      "layernorm param grads bf16 / f32");
-  int64_t ldres = 0;
-  if (dres) {
-    req(dres->sizes() == x.sizes() && is_bf16(*dres), "layernorm residual grad: bf16, shape of x");
-    ldres = rows2d(*dres).ld;
-  }
-  Tensor dx = at::empty(x.sizes(), x.options());
-  const Rows rx = rows2d(dx);
-  void* part = workspace(1024LL * 2 * r.C * 4, x.device(), stream);
-  const int rc = otamd_layernorm_bwd_fused(P(x), r.ld, P(dy), rd.ld, dres ? P(*dres) : nullptr, ldres, P(dx), rx.ld,
-                                           (int)r.rows, (int)r.C, P(gamma), (const float*)P(mean),
-                                           (const float*)P(rstd), P(dgamma), P(dbeta), is_f32(dgamma), param_acc,
-                                           (float*)part, 0, S(stream));
-  if (rc == OTAMD_EUNSUPPORTED) return py::none();
-  check(rc, "otamd_layernorm_bwd_fused");
-  return py::cast(dx);
-}
-
 void layernorm_param_grad(const Tensor& x, const Tensor& dy, const Tensor& mean, const Tensor& rstd,
                           const Tensor& dgamma, const Tensor& dbeta, bool param_acc, int64_t stream) {
   const Rows r = rows2d(x), rd = rows2d(dy);
@@ -583,7 +559,6 @@ PYBIND11_MODULE(_otamd_host, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd_res", &layernorm_bwd_res);
   m.def("layernorm_param_grad", &layernorm_param_grad);
-  m.def("layernorm_bwd_fused", &layernorm_bwd_fused);
   m.def("groupnorm_fwd", &groupnorm_fwd);
   m.def("groupnorm_bwd", &groupnorm_bwd);
   m.def("attn_fwd", &attn_fwd);

@@ -788,138 +788,6 @@ __global__ void __launch_bounds__(512) ln_param_part_kernel(const bf16_t* __rest
   }
 }
 
-// ---- LayerNorm backward + parameter-gradient partials in one pass over x and dy.
-// The row-group body of ln_bwd_rows_kernel, grid-strided so each wave covers several row groups, plus the per-column
-// products dy*xhat (dgamma) and dy (dbeta).  The RPW rows of a wave share their lanes' columns, so each chunk's 16
-// products per lane are reduce-scattered across the row lanes (one v_permlane32 / v_permlane16 swap or xor-shuffle
-// and one add per two values per level) and the lane adds its 16/RPW sums into the wave's running column sums in
-// LDS (registers for all of them pushed an earlier fused attempt to one wave per SIMD, this one's first form into
-// spills).  At the end the four waves' sums meet (fixed order) and the block writes its partial [2][C]; the
-// partials are summed in block order by ln_param_reduce2_kernel.  Every sum has a fixed order: deterministic.
-// Chunk value index q = 8 kind + j (kind 0: dy*xhat, 1: dy; element j).  Level l (row-lane bit o = 32 >> l, while
-// o >= L) pairs entries (2i, 2i+1) -> i; the lane with bit o set keeps the odd one, so after log2(RPW) levels
-// entry i of a lane holds value i * RPW + sel, sel = sum_l bit(o_l) << l.
-__device__ __forceinline__ float rs_pair(float a, float b, int o, int lane) {
-  if (o == 32) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  if (o == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  const bool hi = (lane & o) != 0;
-  return (hi ? b : a) + __shfl_xor(hi ? a : b, o, 64);
-}
-
-template <int CPL, int RPW>
-__global__ void __launch_bounds__(256, 2) ln_bwd_fused_kernel(const bf16_t* __restrict__ x, long long ldx,
-                                                              const bf16_t* __restrict__ dy, long long lddy,
-                                                              bf16_t* __restrict__ dx, long long lddx, int rows, int C,
-                                                              const bf16_t* __restrict__ gamma,
-                                                              const float* __restrict__ mean_in,
-                                                              const float* __restrict__ rstd_in, int accumulate,
-                                                              const bf16_t* __restrict__ res, long long ldres,
-                                                              float* __restrict__ part) {
-  extern __shared__ float red[];   // [4 waves][2][C]: each wave's running column sums
-  constexpr int L = 64 / RPW;
-  constexpr int NA = 16 / RPW;     // per chunk: 16 products -> 16 / RPW sums per lane
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int li = lane & (L - 1);
-  const int C8 = C >> 3;
-  float* mine = red + w * 2 * C;
-  for (int c = lane; c < 2 * C; c += 64) mine[c] = 0.f;   // wave-private: in-order LDS within the wave
-  int sel = 0;   // the lane's reduce-scatter selector (see above)
-  {
-    int l = 0;
-#pragma unroll
-    for (int o = 32; o >= L; o >>= 1, ++l) sel |= ((lane & o) ? 1 : 0) << l;
-  }
-  const bf16_t* add = res ? res : (accumulate ? dx : nullptr);
-  const long long ldadd = res ? ldres : lddx;
-  const long long groups = ((long long)rows + RPW - 1) / RPW;
-  for (long long gi = (long long)blockIdx.x * 4 + w; gi < groups; gi += (long long)gridDim.x * 4) {
-    const long long row = gi * RPW + lane / L;
-    const bool ok = row < rows;
-    const long long rr = ok ? row : 0;
-    const float mean = ok ? mean_in[rr] : 0.f, rstd = ok ? rstd_in[rr] : 0.f;
-    bf8 xr[CPL], dr[CPL], ar[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int c8 = li + L * k;
-      xr[k] = *reinterpret_cast<const bf8*>(x + rr * ldx + c8 * 8);
-      dr[k] = *reinterpret_cast<const bf8*>(dy + rr * lddy + c8 * 8);
-    }
-    if (add) {
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) ar[k] = *reinterpret_cast<const bf8*>(add + rr * ldadd + (li + L * k) * 8);
-    }
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      float xf[8], dv[8], gm[8];
-      unpack8(xr[k], xf);
-      unpack8(dr[k], dv);
-      unpack8(*reinterpret_cast<const bf8*>(gamma + (li + L * k) * 8), gm);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float g = dv[j] * gm[j];
-        s1 += g;
-        s2 = fmaf(g, (xf[j] - mean) * rstd, s2);
-      }
-    }
-    const float m1 = group_sum(s1, L) / C, m2 = group_sum(s2, L) / C;
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {   // re-unpack below rather than keep the first pass's floats live
-      opaque(xr[k]);
-      opaque(dr[k]);
-      if (add) opaque(ar[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int c8 = li + L * k;
-      float xf[8], dv[8], gm[8], o[8];
-      unpack8(xr[k], xf);
-      unpack8(dr[k], dv);
-      unpack8(*reinterpret_cast<const bf8*>(gamma + c8 * 8), gm);
-      float ad[8];
-      if (add) unpack8(ar[k], ad);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = rstd * (dv[j] * gm[j] - m1 - (xf[j] - mean) * rstd * m2);
-        if (add) o[j] += ad[j];
-      }
-      if (ok) *reinterpret_cast<bf8*>(dx + row * lddx + c8 * 8) = pack8(o);
-      // this chunk's parameter-gradient products (dy xhat, dy), reduce-scattered over the wave's rows and added
-      // into the wave's LDS sums in element-major layout [kind][j][c8] (the lanes of one add hit consecutive
-      // words; one lane per address keeps the order fixed; LDS float atomics measured 2x slower here)
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = ok ? dv[j] * ((xf[j] - mean) * rstd) : 0.f;
-        v[8 + j] = ok ? dv[j] : 0.f;
-      }
-#pragma unroll
-      for (int o2 = 32, n = 16; o2 >= L; o2 >>= 1, n >>= 1) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (i < n / 2) v[i] = rs_pair(v[2 * i], v[2 * i + 1], o2, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int q = i * RPW + sel;   // 0..15: kind q >> 3, element q & 7
-        mine[(q >> 3) * C + (q & 7) * C8 + c8] += v[i];
-      }
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < 2 * C; c += 256) {   // part [2][C] in channel order; red in [2][8][C8]
-    const int kind = c >= C, cc = c - kind * C;
-    const int e = kind * C + (cc & 7) * C8 + (cc >> 3);
-    part[(long long)blockIdx.x * 2 * C + c] = ((red[e] + red[2 * C + e]) + red[4 * C + e]) + red[6 * C + e];
-  }
-}
-
 // chunks per lane for a row of C8 16-byte chunks: L = C8 / CPL a power of two <= 64 (0: no fit)
 static int ln_pick(int C8, int* L) {
   const int cands[] = {5, 4, 3, 6, 2, 8, 1};
@@ -1144,65 +1012,6 @@ OTAMD_API int otamd_layernorm_bwd(const void* x, long long ldx, const void* dy, 
   OTAMD_CHECK_LAUNCH();
   if (!dgamma) return OTAMD_OK;
   ln_param_reduce_kernel<<<(2 * C + 31) / 32, 256, 0, stream>>>(part, nb, C, dgamma, dbeta, param_f32, param_acc);
-  OTAMD_CHECK_LAUNCH();
-  return OTAMD_OK;
-}
-
-static int g_ln_fused_blocks = -1;
-// blocks of the fused LayerNorm backward: per-block partials [2][C] are summed by a second small kernel, so fewer
-// blocks = less partial traffic, more row groups per wave.  OTAMD_LN_BLOCKS overrides (A/B).
-static int ln_fused_blocks(long long groups) {
-  if (g_ln_fused_blocks < 0) {
-    const char* e = getenv("OTAMD_LN_BLOCKS");
-    g_ln_fused_blocks = e ? atoi(e) : 512;
-  }
-  const long long need = (groups + 3) / 4, cap = g_ln_fused_blocks > 0 ? g_ln_fused_blocks : 512;
-  return (int)(need < cap ? (need > 0 ? need : 1) : cap);
-}
-
-// dx = LayerNorm-backward(dy) (+ dres, or + dx when accumulate) and dgamma / dbeta from the same read of x and dy
-// (ln_bwd_fused_kernel + ln_param_reduce2_kernel).  dres nullable.  part: float scratch >= 1024 * 2 * C.
-// Widths without a row-group form (C / 8 not CPL x a power of two): OTAMD_EUNSUPPORTED, nothing launched.
-OTAMD_API int otamd_layernorm_bwd_fused(const void* x, long long ldx, const void* dy, long long lddy, const void* dres,
-                                        long long ldres, void* dx, long long lddx, int rows, int C, const void* gamma,
-                                        const float* mean, const float* rstd, void* dgamma, void* dbeta, int param_f32,
-                                        int param_acc, float* part, int accumulate, hipStream_t stream) {
-  if (!x || !dy || !dx || !gamma || !mean || !rstd || !dgamma || !dbeta || !part) return OTAMD_EINVAL;
-  if (rows <= 0 || C % 8 || C > 64 * 8 * LN_MAXCH || ldx % 8 || lddy % 8 || lddx % 8 || (dres && ldres % 8))
-    return OTAMD_EINVAL;
-  if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)dres | (uintptr_t)gamma) & 15) return OTAMD_EINVAL;
-  int L = 0;
-  const int cpl = ln_pick(C / 8, &L);
-  if (!cpl) return OTAMD_EUNSUPPORTED;
-  const int rpw = 64 / L;
-  const long long groups = ((long long)rows + rpw - 1) / rpw;
-  const int nb = ln_fused_blocks(groups);
-  if (nb > 1024) return OTAMD_EINVAL;
-  const size_t lds = (size_t)4 * 2 * C * sizeof(float);
-  const bf16_t* xr = (const bf16_t*)x;
-  const bf16_t* dyr = (const bf16_t*)dy;
-  const bf16_t* rr = (const bf16_t*)dres;
-  const bf16_t* gr = (const bf16_t*)gamma;
-  bf16_t* dxr = (bf16_t*)dx;
-#define LNBF(K, R) ln_bwd_fused_kernel<K, R><<<nb, 256, lds, stream>>>(xr, ldx, dyr, lddy, dxr, lddx, rows, C, gr, mean, \
-                                                                      rstd, accumulate, rr, ldres, part)
-  bool launched = true;
-  if (cpl == 5 && rpw == 2) LNBF(5, 2);
-  else if (cpl == 5 && rpw == 4) LNBF(5, 4);
-  else if (cpl == 5 && rpw == 8) LNBF(5, 8);
-  else if (cpl == 4 && rpw == 1) LNBF(4, 1);
-  else if (cpl == 4 && rpw == 2) LNBF(4, 2);
-  else if (cpl == 4 && rpw == 4) LNBF(4, 4);
-  else if (cpl == 3 && rpw == 2) LNBF(3, 2);
-  else if (cpl == 3 && rpw == 4) LNBF(3, 4);
-  else if (cpl == 6 && rpw == 2) LNBF(6, 2);
-  else if (cpl == 2 && rpw == 2) LNBF(2, 2);
-  else if (cpl == 2 && rpw == 4) LNBF(2, 4);
-  else launched = false;
-#undef LNBF
-  if (!launched) return OTAMD_EUNSUPPORTED;
-  OTAMD_CHECK_LAUNCH();
-  ln_param_reduce2_kernel<<<(2 * C + 15) / 16, 1024, 0, stream>>>(part, nb, C, dgamma, dbeta, param_f32, param_acc);
   OTAMD_CHECK_LAUNCH();
   return OTAMD_OK;
 }

@@ -657,12 +657,35 @@ def adamw_f32(p, g, m, v, groups, clip_coef=None):
           "otamd_adamw_f32")
 
 
-def grad_clip_coef(grads, chunks_dev, n_chunks, chunk_sq, tensor_sq, n_tensors, max_norm, out):
+def adamw_master(p32, g, m32, v32, w, groups, clip_coef=None, begin=0, end=None):
+    """fp32-master AdamW over elements [begin, end): fp32 p / m / v, bf16 gradients in, the bf16 working copy w
+    rewritten as rne(p) (util/optimizer/adamw_fused.py, master stores)."""
+    n = p32.numel()
+    end = n if end is None else end
+    for t in (p32, m32, v32):
+        _req(t.dtype == F32 and t.is_contiguous() and t.numel() == n and _aligned(t), "adamw master f32 buffers")
+    for t in (g, w):
+        _req(t.dtype == BF16 and t.is_contiguous() and t.numel() == n and _aligned(t), "adamw master bf16 buffers")
+    _req(0 <= begin <= end <= n and begin % 8 == 0 and end % 8 == 0, "adamw range: multiples of 8 within the store")
+    arr = (_lib.AdamwGroup * len(groups))(*groups)
+    check(lib().otamd_adamw_master_range(_p(p32), _p(g), _p(m32), _p(v32), _p(w), begin, end, arr, len(groups),
+                                         _p(clip_coef), stream_handle()),
+          "otamd_adamw_master_range")
+
+
+def grad_norm_dtype(grads, fp32_semantics=False):
+    """the C-ABI grad_dtype code: 0 bf16, 1 fp32, 2 bf16 storage of an fp32-master network's gradients."""
+    if grads.dtype == BF16:
+        return 2 if fp32_semantics else 0
+    return 1
+
+
+def grad_clip_coef(grads, chunks_dev, n_chunks, chunk_sq, tensor_sq, n_tensors, max_norm, out, fp32_semantics=False):
     _req(grads.dtype in (BF16, F32) and grads.is_contiguous(), "grads flat")
     _req(chunk_sq.dtype == torch.float64 and chunk_sq.numel() >= n_chunks, "chunk_sq f64")
     _req(tensor_sq.dtype == torch.float64 and tensor_sq.numel() >= n_tensors, "tensor_sq f64")
     _req(out.dtype == F32 and out.numel() >= 2, "out f32[2]")
-    check(lib().otamd_grad_clip_coef(_p(grads), 0 if grads.dtype == BF16 else 1, _p(chunks_dev), n_chunks,
+    check(lib().otamd_grad_clip_coef(_p(grads), grad_norm_dtype(grads, fp32_semantics), _p(chunks_dev), n_chunks,
                                      _p(chunk_sq), _p(tensor_sq), n_tensors, float(max_norm), _p(out),
                                      stream_handle()),
           "otamd_grad_clip_coef")
@@ -804,32 +827,6 @@ def layernorm_bwd_res(x, dy, dres, gamma, stats):
         layernorm_bwd(x, dy, gamma, stats, dx=dx, need_param_grads=False)
         return add(dx, dres, out=dx)
     check(rc, "otamd_layernorm_bwd_res")
-    return dx
-
-
-def layernorm_bwd_fused(x, dy, gamma, stats, dgamma, dbeta, dres=None, param_acc=False):
-    """dx = LayerNorm-backward(dy) (+ dres) and dgamma / dbeta (= or +=) from one read of x and dy; None when the
-    width has no fused form (the caller then runs layernorm_bwd(_res) + layernorm_param_grad)."""
-    h = _host()
-    if h is not None:
-        return h.layernorm_bwd_fused(x, dy, dres, gamma, stats[0], stats[1], dgamma, dbeta, param_acc, stream_handle())
-    rows, C_, ldx = _rows2d(x)
-    _, _, lddy = _rows2d(dy)
-    _req(dgamma.dtype == dbeta.dtype and dgamma.dtype in (BF16, F32), "layernorm param grads bf16 / f32")
-    ldres = 0
-    if dres is not None:
-        _req(dres.shape == x.shape and dres.dtype == BF16, "layernorm residual grad: bf16, shape of x")
-        _, _, ldres = _rows2d(dres)
-    dx = torch.empty(x.shape, dtype=BF16, device=x.device)
-    _, _, lddx = _rows2d(dx)
-    part = workspace(1024 * 2 * C_ * 4, x.device)
-    mean, rstd = stats
-    rc = lib().otamd_layernorm_bwd_fused(_p(x), ldx, _p(dy), lddy, _p(dres) if dres is not None else None, ldres,
-                                         _p(dx), lddx, rows, C_, _p(gamma), _p(mean), _p(rstd), _p(dgamma), _p(dbeta),
-                                         int(dgamma.dtype == F32), int(param_acc), _p(part), 0, stream_handle())
-    if rc == 3:   # OTAMD_EUNSUPPORTED
-        return None
-    check(rc, "otamd_layernorm_bwd_fused")
     return dx
 
 

@@ -150,14 +150,14 @@ def rope_tables(L: int, h: int, w: int, cfg: FluxConfig):
 
 class FluxTransformer2DModel:
     def __init__(self, cfg: FluxConfig, device, dtype=BF16, seed: int | None = 0, group: str = "transformer",
-                 trainable: bool = True):
+                 trainable: bool = True, master: bool = False):
         if cfg.attention_head_dim != 128 or sum(cfg.axes_dims_rope) != 128:
             raise NotImplementedError("the q/k norm + RoPE kernel is built for 128-wide heads")
         self.cfg = cfg
         self.device = torch.device(device)
         self.specs = flux_specs(cfg)
         self.store = FlatParamStore([(n, sh, group) for n, sh, _, _ in self.specs], dtype, self.device,
-                                    trainable=trainable)
+                                    trainable=trainable, master=master)
         self.config = {"guidance_embeds": cfg.guidance_embeds}
         self.lora = None
         self._refs: dict = {}
@@ -181,9 +181,9 @@ class FluxTransformer2DModel:
                 p = self.store.params[name]
                 if kind in ("linear", "bias"):
                     b = 1.0 / math.sqrt(fan_in)
-                    p.copy_(((torch.rand(shape, generator=g, device=self.device) * 2 - 1) * b).to(p.dtype))
+                    self.store.write(name, (torch.rand(shape, generator=g, device=self.device) * 2 - 1) * b)
                 else:
-                    p.fill_(1.0)
+                    self.store.write(name, torch.ones_like(p))
 
     def parameters(self):
         return [p for _, p in self.store.named_parameters()]
@@ -195,7 +195,7 @@ class FluxTransformer2DModel:
         self.store.wait_params()
         out = {}
         for name, *_ in self.specs:
-            v = self.store.params[name].grad if grads else self.store.params[name].detach()
+            v = self.store.params[name].grad if grads else self.store.value(name)
             out[name] = v.to(dtype or v.dtype).contiguous()
         return out
 
@@ -204,7 +204,7 @@ class FluxTransformer2DModel:
             for name, shape, *_ in self.specs:
                 if tuple(sd[name].shape) != tuple(shape):
                     raise ValueError(f"{name}: shape {tuple(sd[name].shape)} != {shape}")
-                self.store.params[name].copy_(sd[name].to(self.device, self.store.dtype))
+                self.store.write(name, sd[name].to(self.device, torch.float32))
 
     def R(self, names, shape=None) -> Fn.PRef:
         key = (tuple(names) if isinstance(names, (list, tuple)) else names, shape)

@@ -389,13 +389,6 @@ def group_norm_res(x, gref, bref, groups, eps, silu):
     return GroupNormResFn.apply(x, gref, bref, groups, eps, silu, *_params(gref, bref))
 
 
-# LayerNorm backward as one pass producing dx and dgamma / dbeta (otamd_layernorm_bwd_fused): opt-in
-# (OTAMD_LN_FUSED=1).  It saves a read of x and dy but runs at 2 waves per SIMD against the row pass's 3 and measured
-# 32.6 vs 27.9 us (4096 x 1280) and 43.0 vs 44.9 us (16384 x 640) for row pass + parameter pass, cold
-# (tools/ln_bench.py, profiles/r5_ln_bench.jsonl), so the two-pass form stays the default.
-_LN_FUSED = os.environ.get("OTAMD_LN_FUSED", "0") == "1"
-
-
 class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gref, bref, eps, *params):
@@ -410,12 +403,6 @@ class LayerNormFn(torch.autograd.Function):
         if dy.stride(-1) != 1:
             dy = dy.contiguous()
         tr = ctx.gref.trainable
-        if tr and _LN_FUSED:   # dx, dgamma and dbeta from one read of x and dy
-            dx = K.layernorm_bwd_fused(x, dy, ctx.gref.w, stats, ctx.gref.g, ctx.bref.g, param_acc=ctx.gref.acc())
-            if dx is not None:
-                ctx.gref.done()
-                ctx.bref.done()
-                return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
         if tr:   # dgamma / dbeta only feed the optimizer: side stream, like the GEMM weight gradients
             with S.wgrad_region((x, dy, *stats)):
                 K.layernorm_param_grad(x, dy, stats, ctx.gref.g, ctx.bref.g, param_acc=ctx.gref.acc())
@@ -449,15 +436,6 @@ class LayerNormResFn(torch.autograd.Function):
         if dy.stride(-1) != 1:
             dy = dy.contiguous()
         tr = ctx.gref.trainable
-        if tr and _LN_FUSED:   # dx (+ the residual gradient), dgamma and dbeta from one read of x and dy
-            if dres is not None and (dres.stride(-1) != 1 or not dres.is_contiguous()):
-                dres = dres.contiguous()
-            dx = K.layernorm_bwd_fused(x, dy, ctx.gref.w, stats, ctx.gref.g, ctx.bref.g, dres=dres,
-                                       param_acc=ctx.gref.acc())
-            if dx is not None:
-                ctx.gref.done()
-                ctx.bref.done()
-                return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
         if dres is None:
             dx, _, _ = K.layernorm_bwd(x, dy, ctx.gref.w, stats, need_param_grads=False)
         else:

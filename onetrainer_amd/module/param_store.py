@@ -27,10 +27,14 @@ class Slot:
 
 
 class FlatParamStore:
-    def __init__(self, specs, dtype, device, align_bytes=16, trainable=True):
+    def __init__(self, specs, dtype, device, align_bytes=16, trainable=True, master=False):
         """specs: iterable of (name, shape, group) in layout order.  trainable=False: a frozen base
         (LoRA training, unet.requires_grad_(False) in StableDiffusionXLLoRASetup.py:78-86): no grad
-        buffer, parameters do not require grad, backward kernels skip its weight gradients."""
+        buffer, parameters do not require grad, backward kernels skip its weight gradients.
+        master=True: fp32 master weights (weight_dtype FLOAT_32, TrainConfig.py:782) behind the bf16 working copy
+        `data` the kernels read -- `master` holds the trained values, `data` their round-to-nearest bf16 cast (what
+        autocast feeds every GEMM, dtype_util.py:28-49); gradients stay bf16 (autocast's weight gradients are bf16
+        GEMM results cast to fp32, so bf16 holds them exactly)."""
         esz = torch.tensor([], dtype=dtype).element_size()
         al = max(8, align_bytes // esz)   # >= 8 elements: the grad-norm kernel reads 8-wide chunks
         self.dtype, self.device = dtype, device
@@ -48,6 +52,9 @@ class FlatParamStore:
         self.numel = (off + al - 1) // al * al
         self.trainable = trainable
         self.data = torch.zeros(self.numel, dtype=dtype, device=device)
+        if master and (not trainable or dtype != torch.bfloat16):
+            raise ValueError("fp32 master weights back a trainable bf16 store")
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=device) if master else None
         self.grad = torch.zeros(self.numel, dtype=dtype, device=device) if trainable else None
         self._params: dict[str, torch.nn.Parameter] = {}
         for name in self.order:
@@ -97,6 +104,26 @@ class FlatParamStore:
         elif len(names) == 1:
             v = v.view(first.shape)
         return v
+
+    def value(self, name):
+        """the trained value of one tensor (store layout): the fp32 master view, else the parameter view."""
+        s = self.slots[name]
+        if self.master is not None:
+            return self.master[s.offset:s.offset + s.numel].view(s.shape)
+        return self.params[name].detach()
+
+    @torch.no_grad()
+    def write(self, name, value):
+        """set one tensor (store layout); with master weights the fp32 value goes to the master and the working
+        copy takes its bf16 cast."""
+        s = self.slots[name]
+        if self.master is not None:
+            self.wait_params()
+            mv = self.master[s.offset:s.offset + s.numel].view(s.shape)
+            mv.copy_(value)
+            self.data[s.offset:s.offset + s.numel].view(s.shape).copy_(mv)
+        else:
+            self.params[name].copy_(value)
 
     def range_of(self, names):
         first = self.slots[names[0]]

@@ -227,13 +227,13 @@ class UNet2DConditionModel:
     """HIP UNet; parameters live in `self.store` (FlatParamStore)."""
 
     def __init__(self, cfg: UNetConfig, device, dtype=BF16, seed: int | None = 0, group: str = "unet",
-                 trainable: bool = True):
+                 trainable: bool = True, master: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
         self.specs = unet_specs(cfg)
         self.store = FlatParamStore([(n, _store_shape(n, sh, k, cfg), group) for n, sh, k, _ in self.specs],
-                                    dtype, self.device, trainable=trainable)
+                                    dtype, self.device, trainable=trainable, master=master)
         self._refs: dict = {}
         self.lora = None      # module/lora.py LoRAUNetWrapper when training adapters on a frozen base
         if seed is not None:
@@ -251,9 +251,9 @@ class UNet2DConditionModel:
                     val = (torch.rand(shape, generator=g, device=self.device) * 2 - 1) * bound
                     self._assign(name, val, kind)
                 elif kind == "norm_w":
-                    p.fill_(1.0)
+                    self.store.write(name, torch.ones_like(p))
                 else:
-                    p.zero_()
+                    self.store.write(name, torch.zeros_like(p))
 
     def _assign(self, name, val_diffusers, kind):
         p = self.store.params[name]
@@ -266,7 +266,7 @@ class UNet2DConditionModel:
                 v = torch.nn.functional.pad(v, (0, 0, 0, 0, 0, 0, 0, PAD_OUT - v.shape[0]))
         if name == "conv_out.bias":
             v = torch.nn.functional.pad(v, (0, PAD_OUT - v.shape[0]))
-        p.data.copy_(v.to(p.dtype))
+        self.store.write(name, v)
 
     def named_parameters(self):
         return self.store.named_parameters()
@@ -282,7 +282,7 @@ class UNet2DConditionModel:
         """diffusers-layout state dict (NCHW conv weights, unpadded); grads=True exports gradients."""
         out = {}
         for name, shape, kind, _ in self.specs:
-            v = self.store.params[name].grad if grads else self.store.params[name].detach()
+            v = self.store.params[name].grad if grads else self.store.value(name)
             if kind == "conv":
                 if v.dim() == 2:
                     v = v.reshape(v.shape[0], v.shape[1], 1, 1)

@@ -103,18 +103,18 @@ class GenericTrainer(TimedActionMixin):
         self._attach_norm_overlap()
 
     def _attach_norm_overlap(self):
-        """single process, eager steps, clip on, the fused AdamW: clip_grad_norm_'s norm pass runs during backward
-        (util/optimizer/adamw_fused.OverlappedGradNorm); data parallel clips the all-reduced gradients instead."""
+        """eager steps, clip on, the fused AdamW: clip_grad_norm_'s norm pass runs during backward
+        (util/optimizer/adamw_fused.OverlappedGradNorm) -- in one process as gradient ranges finish, under data
+        parallel as the reducer's buckets finish their all-reduce (the norm of the global-mean gradients)."""
         import os
 
         from ..module import streams as S
         from ..util.optimizer.adamw_fused import FusedAdamW, OverlappedGradNorm
         opt = getattr(self.model, "optimizer", None)
-        if (isinstance(opt, FusedAdamW) and self.world == 1 and self.reducer is None and self.graphs is None
-                and self.config.clip_grad_norm
+        if (isinstance(opt, FusedAdamW) and self.graphs is None and self.config.clip_grad_norm
                 and opt.store.grad.is_cuda and S.enabled() and os.environ.get("OTAMD_NORM_OVERLAP", "1") != "0"
                 and opt.norm_overlap is None):
-            opt.norm_overlap = OverlappedGradNorm(opt)
+            opt.norm_overlap = OverlappedGradNorm(opt, reducer=self.reducer)
 
     def _load_weights(self):
         """base / VAE / LoRA weights and a backup to continue from (GenericTrainer.py:92-108 +
@@ -258,11 +258,13 @@ class GenericTrainer(TimedActionMixin):
                 norm.arm(update and cfg.clip_grad_norm is not None)
             loss.backward()
             store.finish_backward()
-            if norm is not None:
+            if norm is not None and not norm.dp:
                 norm.finish()
         if update:
             if self.reducer is not None:
-                self.reducer.finish()
+                self.reducer.finish()   # the last buckets, their norm sums (reduced_hooks), the post stream joined
+                if norm is not None and norm.dp:
+                    norm.finish()
             if cfg.clip_grad_norm is not None:
                 model.optimizer.clip_grad_norm_(cfg.clip_grad_norm)
             model.optimizer.step()

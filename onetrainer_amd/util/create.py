@@ -28,7 +28,7 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
         from ..model.FluxModel import FluxModel
         from ..module import flux as FX
         tr = FX.FluxTransformer2DModel(flux_config or FX.flux_dev_config(), device, seed=seed,
-                                       trainable=config.training_method != "LORA")
+                                       trainable=config.training_method != "LORA", master=plan.master)
         m = FluxModel(tr, model_type=mt)
         m.dtype_plan = plan
         return m
@@ -41,7 +41,8 @@ def create_model(config, device, seed=0, unet_config=None, prediction_type="epsi
             unet_config = U.sd15_config()
         else:
             raise NotImplementedError(f"model type {mt}")
-    unet = U.UNet2DConditionModel(unet_config, device, seed=seed, trainable=config.training_method != "LORA")
+    unet = U.UNet2DConditionModel(unet_config, device, seed=seed, trainable=config.training_method != "LORA",
+                                  master=plan.master)
     ns = NoiseScheduler(device, prediction_type=prediction_type)
     m = StableDiffusionXLModel(unet, ns, SCALING.get(mt, 0.13025), model_type=mt)
     m.dtype_plan = plan

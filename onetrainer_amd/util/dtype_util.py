@@ -12,8 +12,10 @@ Reference (read from the config):
   * defaults (TrainConfig.py:782, 816-817): weight FLOAT_32, train FLOAT_16, fallback BFLOAT_16.
 
 This build's kernels compute in bf16 (MFMA bf16 inputs, fp32 accumulation; norms, softmax and the loss in
-fp32) and store the trained network in bf16 (full fine-tune) or keep a frozen bf16 base plus fp32 adapters
-(LoRA).  `dtype_plan(cfg)` maps a config onto that:
+fp32) and store the trained network in bf16 (full fine-tune, bf16 weights), in fp32 master weights behind a bf16
+working copy (full fine-tune, FLOAT_32 weights: module/param_store.py `master`, csrc/adamw.hip
+adamw_master_kernel), or keep a frozen bf16 base plus fp32 adapters (LoRA).  `dtype_plan(cfg)` maps a config
+onto that:
   * the same decision as the reference -> taken;
   * a decision that only changes precision in a direction the build supports -> taken with an OVERRIDE
     record (field, reference value, build value, reason), logged once by the trainer and kept on the model
@@ -21,9 +23,13 @@ fp32) and store the trained network in bf16 (full fine-tune) or keep a frozen bf
     base in FLOAT_16 / FLOAT_32 / a quantized format -> stored BFLOAT_16 (autocast casts frozen weights to the
     compute dtype anyway; NF4 / int8 need bitsandbytes, CUDA-only); bf16 / fp16 adapters -> kept fp32; the
     reference's GradScaler -> not needed with bf16 compute;
-  * a decision the build cannot honour -> ValueError before any weight is allocated: fp32 master weights for
-    full fine-tune (TrainConfig.default_values() and the SD 1.5 preset), fp32 / tf32 compute, a trained network
-    in a quantized format.
+  * a decision the build cannot honour -> ValueError before any weight is allocated: fp32 / tf32 compute, a
+    trained network in a quantized format.
+fp32 master weights for a full fine-tune (TrainConfig.default_values() and the SD 1.5 preset) are honoured: the
+reference holds fp32 weights and autocast casts them to bf16 (round to nearest) for every GEMM, and their
+gradients are those bf16 GEMM results cast to fp32; the build keeps fp32 p / m / v, bf16 gradients and a bf16
+working copy rewritten by the optimizer launch.  One deviation is recorded: norm-layer gradients, which autocast
+computes in fp32 (group_norm / layer_norm run in fp32), are rounded to bf16 by the shared gradient store.
 """
 from __future__ import annotations
 
@@ -81,6 +87,7 @@ class DtypePlan:
     compute: str = BF16
     network: str = BF16            # trained (fine-tune) or frozen (LoRA) network storage
     adapters: str | None = None    # LoRA adapter storage
+    master: bool = False           # fp32 master weights behind a bf16 working copy (full fine-tune, FLOAT_32)
     overrides: list = field(default_factory=list)   # [{field, reference, build, reason}]
 
     def summary(self) -> str:
@@ -100,8 +107,8 @@ def dtype_plan(cfg) -> DtypePlan:
 
     c = ref["compute"]
     if c in ("FLOAT_32", "TFLOAT_32"):
-        raise ValueError(f"train_dtype {c}: this build computes the network in bf16 MFMA kernels (fp32 compute is not "
-                         f"built); set train_dtype to BFLOAT_16")
+        raise ValueError(f"train_dtype {c}: this build computes the network in bf16 MFMA kernels, fp32 compute is not "
+                         f"built; set train_dtype to BFLOAT_16")
     if c == "FLOAT_16":
         plan.overrides.append({"field": "train_dtype", "reference": c, "build": BF16,
                                "reason": "bf16 MFMA kernels, same rate as fp16, fp32 exponent range (SURVEY.md §8(d) C3)"})
@@ -111,12 +118,13 @@ def dtype_plan(cfg) -> DtypePlan:
     n = ref["network"]
     if not lora:
         if n == "FLOAT_32":
-            raise ValueError(f"{net_field} / weight_dtype FLOAT_32: full fine-tune with fp32 master weights is not built "
-                             f"(the trained network is stored in bf16 with stochastic rounding); set weight_dtype to "
-                             f"BFLOAT_16")
-        if n in QUANTIZED:
+            plan.network, plan.master = "FLOAT_32", True
+            plan.overrides.append({"field": "norm gradients", "reference": "FLOAT_32", "build": BF16,
+                                   "reason": "fp32 master weights; GroupNorm / LayerNorm weight gradients pass through "
+                                             "the bf16 gradient store (every GEMM gradient is bf16-exact anyway)"})
+        elif n in QUANTIZED:
             raise ValueError(f"{net_field} {n}: a quantized network cannot be fine-tuned")
-        if n == "FLOAT_16":
+        elif n == "FLOAT_16":
             plan.overrides.append({"field": net_field, "reference": n, "build": BF16,
                                    "reason": "bf16 storage of the trained network (no fp16 kernels)"})
         elif n != BF16:

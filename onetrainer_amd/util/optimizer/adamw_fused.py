@@ -40,8 +40,12 @@ class FusedAdamW(torch.optim.Optimizer):
         self.store = store
         self.stochastic_rounding = stochastic_rounding
         self.seed = seed
-        self.exp_avg = torch.zeros_like(store.data)
-        self.exp_avg_sq = torch.zeros_like(store.data)
+        # fp32 master weights (module/param_store.py `master`): fp32 moments, the reference's fp32 AdamW path
+        # (adamw_extensions.py:125-148 without stochastic rounding, which applies to bf16 parameters only)
+        self.master = getattr(store, "master", None)
+        self.exp_avg = torch.zeros_like(self.master if self.master is not None else store.data)
+        self.exp_avg_sq = torch.zeros_like(self.exp_avg)
+        self._norm_dtype = K.grad_norm_dtype(store.grad, self.master is not None) if store.grad is not None else 0
         self._ptr2name = {store.params[n].data_ptr(): n for n in store.order}
         self._ranges = []
         for g in self.param_groups:
@@ -76,7 +80,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.norm_overlap = None   # OverlappedGradNorm, attached by the trainer (single process, clip on)
         # overlapped update: chunk boundaries on tensor boundaries, ~numel / 16 each
         self.overlap = (store.device.type == "cuda" and store.dtype == torch.bfloat16 and store.numel >= (1 << 26)
-                        and os.environ.get("OTAMD_OPT_OVERLAP", "0") == "1")
+                        and self.master is None and os.environ.get("OTAMD_OPT_OVERLAP", "0") == "1")
         self._opt_chunks = []
         if self.overlap:
             target = store.numel // 16
@@ -99,13 +103,12 @@ class FusedAdamW(torch.optim.Optimizer):
         if self.norm_overlap is not None and self.norm_overlap.take():   # sums accumulated during backward
             _lib.check(_lib.lib().otamd_grad_clip_finalize(self._chunks.data_ptr(), self._n_chunks,
                                                            self._chunk_sq.data_ptr(), self._tensor_sq.data_ptr(), nt,
-                                                           float(max_norm),
-                                                           0 if self.store.grad.dtype == torch.bfloat16 else 1,
+                                                           float(max_norm), self._norm_dtype,
                                                            self.clip_out.data_ptr(), K.stream_handle()),
                        "otamd_grad_clip_finalize")
         else:
             K.grad_clip_coef(self.store.grad, self._chunks, self._n_chunks, self._chunk_sq, self._tensor_sq, nt,
-                             max_norm, self.clip_out)
+                             max_norm, self.clip_out, fp32_semantics=self.master is not None)
         self._pending_clip = True
         return self.clip_out[1]
 
@@ -142,7 +145,9 @@ class FusedAdamW(torch.optim.Optimizer):
         clip = self.clip_out if getattr(self, "_pending_clip", False) else None
         self._pending_clip = False
         st = self.store
-        if st.dtype == torch.bfloat16:
+        if self.master is not None:
+            K.adamw_master(self.master, st.grad, self.exp_avg, self.exp_avg_sq, st.data, groups, clip_coef=clip)
+        elif st.dtype == torch.bfloat16:
             self.seed = (self.seed * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
             if self.overlap:
                 st.wait_params()                                   # a previous update still in flight
@@ -180,8 +185,12 @@ class FusedAdamW(torch.optim.Optimizer):
         finally:
             self._ranges[gi] = saved
         st = self.store
+        b, e = s.offset // 8 * 8, (s.offset + s.numel + 7) // 8 * 8   # this tensor only (the store pads to 8)
+        if self.master is not None:
+            K.adamw_master(self.master, st.grad, self.exp_avg, self.exp_avg_sq, st.data, groups, begin=b, end=e)
+            return
         K.adamw_bf16(st.data, st.grad, self.exp_avg, self.exp_avg_sq, groups, clip_coef=None,
-                     stochastic_rounding=self.stochastic_rounding, seed=self.seed)
+                     stochastic_rounding=self.stochastic_rounding, seed=self.seed, begin=b, end=e)
 
     def zero_grad(self, set_to_none: bool = True):
         """grads are views of the flat store that the next backward overwrites; nothing to clear."""
@@ -230,7 +239,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
 
 class OverlappedGradNorm:
-    """clip_grad_norm_'s squared-norm pass spread over the backward (single process): gradient ranges of about
+    """clip_grad_norm_'s squared-norm pass spread over the backward.  Single process: gradient ranges of about
     `bucket_bytes` (whole tensors, reverse layout order = the order backward finishes them) are summed on the
     weight-gradient stream as soon as every tensor in the range has its gradient -- the stream then waits for
     the dgrad chain's position, so both streams' writes are ordered before the read.  clip_grad_norm_ then only
@@ -238,10 +247,14 @@ class OverlappedGradNorm:
     the whole gradient buffer (SDXL: 5.1 GB, ~0.9 ms) after backward.  The sums are fp64, one slot per chunk
     (no atomics: the same bits every run), and the coefficient is formed with torch's bf16 roundings exactly as
     otamd_grad_clip_coef does.  Ranges with a tensor that received no gradient are
-    summed after finish_backward has zeroed it.  OTAMD_NORM_OVERLAP=0 disables it."""
+    summed after finish_backward has zeroed it.  Data parallel (`reducer`): the norm must see the all-reduced
+    gradients, so the ranges are the reducer's buckets and each is summed on the reducer's post stream right after
+    its collective completes (trainer/ddp.py reduced_hooks); only the last bucket's sums follow the backward.
+    OTAMD_NORM_OVERLAP=0 disables it."""
 
-    def __init__(self, opt: FusedAdamW, bucket_bytes: int = 64 << 20):
+    def __init__(self, opt: FusedAdamW, bucket_bytes: int = 64 << 20, reducer=None):
         self.opt = opt
+        self.dp = reducer is not None
         store = opt.store
         limit = max(1, bucket_bytes // store.grad.element_size())
         t_chunks: dict = {}
@@ -249,6 +262,16 @@ class OverlappedGradNorm:
             b, e = t_chunks.get(ti, (ci, ci))
             t_chunks[ti] = (min(b, ci), max(e, ci + 1))
         self.buckets = []   # (first chunk, end chunk, names)
+        if self.dp:
+            t_index = {n: ti for ti, n in enumerate(store.order)}
+            for _, _, names in reducer.buckets:
+                spans = [t_chunks[t_index[n]] for n in names if t_index[n] in t_chunks]
+                self.buckets.append((min(b for b, _ in spans) if spans else None,
+                                     max(e for _, e in spans) if spans else None, list(names)))
+            self.armed = False
+            self.ready = False
+            reducer.reduced_hooks.append(self._on_reduced)
+            return
         cur, c_lo, c_hi, size = [], None, None, 0
         for ti in reversed(range(len(store.order))):
             name = store.order[ti]
@@ -286,7 +309,7 @@ class OverlappedGradNorm:
             return
         opt = self.opt
         g = opt.store.grad
-        dtype = 0 if g.dtype == torch.bfloat16 else 1
+        dtype = opt._norm_dtype
         if side is not None:
             from ...module import streams as S
             S.defer_flush()   # the bucket's deferred split-K reduces (module/streams.py) before its norms
@@ -300,6 +323,11 @@ class OverlappedGradNorm:
             _lib.check(_lib.lib().otamd_grad_sqnorm_chunks(g.data_ptr(), dtype, opt._chunks.data_ptr(), c0, c1,
                                                            opt._chunk_sq.data_ptr(), K.stream_handle()),
                        "otamd_grad_sqnorm_chunks")
+
+    def _on_reduced(self, bi):
+        """data parallel: bucket bi holds the global sum (on the reducer's post stream, the current stream here)."""
+        if self.armed:
+            self._launch(bi, None)
 
     def _on_ready(self, names):
         if not self.armed:
@@ -318,6 +346,8 @@ class OverlappedGradNorm:
             return
         for bi in range(len(self.buckets)):
             if not self.launched[bi]:
+                if self.dp:   # every reducer bucket goes out in reducer.finish(), which runs before this
+                    raise RuntimeError("overlapped grad norm: bucket %d was not all-reduced this step" % bi)
                 self._launch(bi, None)
         # every chunk slot is rewritten on an armed step: the finalize never sees an earlier step's sums
         assert all(self.launched), "overlapped grad norm: a bucket was not summed this step"

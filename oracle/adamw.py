@@ -100,6 +100,23 @@ def adamw_step_f32(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weigh
     return p.astype(np.float32), m.astype(np.float32), v.astype(np.float32)
 
 
+def adamw_step_master(p, g_bits, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, clip_coef=None):
+    """fp32 master weights under a bf16 autocast (weight_dtype FLOAT_32, TrainConfig.py:782): the fp32 step on the
+    fp32 value of a bf16 gradient; returns (p, m, v) fp32 and the bits of the bf16 working copy rne(p) (autocast's
+    cast of the weight at the next forward)."""
+    p, m, v = adamw_step_f32(p, bf16_to_f32(g_bits), m, v, step, lr, beta1, beta2, eps, weight_decay, clip_coef)
+    return p, m, v, f32_to_bf16_bits(p)
+
+
+def clip_grad_norm_f32(grads: list[np.ndarray], max_norm=1.0):
+    """torch clip_grad_norm_ on fp32 grads: per-tensor fp32 norms, their fp32 2-norm, coef = max_norm / (total + 1e-6)
+    clamped to 1, in fp32.  (torch sums in fp32 with its own order; the sums here are fp64, rounded once.)"""
+    norms = np.array([np.float32(np.sqrt(np.sum(np.asarray(g, np.float64) ** 2))) for g in grads], np.float32)
+    total = np.float32(np.sqrt(np.sum(norms.astype(np.float64) ** 2)))
+    coef = np.float32(min(np.float32(max_norm) / (total + np.float32(1e-6)), np.float32(1.0)))
+    return float(total), coef
+
+
 def clip_grad_norm_bf16(grads_bits: list[np.ndarray], max_norm=1.0):
     """torch clip_grad_norm_ on bf16 grads: per-tensor norms (bf16), total (bf16), coef (bf16).
     Returns (clipped grads bits, total norm, coef)."""

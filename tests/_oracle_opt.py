@@ -5,7 +5,10 @@ The reference steps bf16 parameters with bf16 grads, moments and the patched Ada
 clip_grad_norm_ on the bf16 grads (GenericTrainer.py:712-713).  OracleBF16AdamW reproduces that on
 an fp32 oracle network whose parameters hold bf16 values: grads are rounded to bf16 (the param
 dtype), clipped with the bf16 clip restatement and stepped with oracle.adamw.adamw_step_bf16.
-OracleF32AdamW is the fp32 (LoRA adapter) case with adamw_step_f32.
+OracleF32AdamW is the fp32 (LoRA adapter) case with adamw_step_f32.  OracleMasterAdamW is a full fine-tune with
+fp32 weights under a bf16 autocast (weight_dtype FLOAT_32, TrainConfig.py:782): each weight gradient is a bf16 GEMM
+result cast to fp32 (rounded to bf16 here, as the build's gradient store holds it), clip_grad_norm_ in fp32 (torch's
+own), adamw_step_f32.
 """
 import numpy as np
 import torch
@@ -66,3 +69,12 @@ class OracleF32AdamW:
                                                          self.wd, clip_coef=coef)
             p.copy_(torch.from_numpy(pn).view_as(p))
             p.grad = None
+
+
+class OracleMasterAdamW(OracleF32AdamW):
+    @torch.no_grad()
+    def step(self):
+        for p in self.params:
+            if p.grad is not None:
+                p.grad.copy_(p.grad.bfloat16().float())
+        super().step()

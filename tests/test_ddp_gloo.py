@@ -112,6 +112,80 @@ def test_bucket_allreduce_grad_accumulation_gloo_world2(reduce_fp32):
     assert res == {0: "ok", 1: "ok"}, res
 
 
+def _worker_norm(rank, world, port, q):
+    """the clip norm under data parallel (util/optimizer/adamw_fused.OverlappedGradNorm(reducer=...)): its ranges are
+    the reducer's buckets and each is summed from the reducer's completion hook -- every norm chunk exactly once per
+    update step, after its bucket holds the global sum, never on a GA micro-step (CPU: the hooks run in finish(); on
+    the GPU on the reducer's post stream, tests/test_dp_gpu.py)"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from onetrainer_amd.util.optimizer.adamw_fused import FusedAdamW, OverlappedGradNorm
+        specs = SPECS + [("big", (70000,), "g")]   # one tensor of two norm chunks (64 K elements each)
+        st = FlatParamStore(specs, torch.bfloat16, torch.device("cpu"))
+        red = GradBucketReducer(st, bucket_bytes=2048)
+        opt = FusedAdamW(st, [{"params": [st.params[n] for n, *_ in specs]}])
+        norm = OverlappedGradNorm(opt, reducer=red)
+        assert norm.dp and len(norm.buckets) == len(red.buckets)
+        chunks = [(b, e) for b, e, _ in (tuple(x) for x in _chunk_table(opt))]
+        hits = []
+
+        def fake_launch(bi, side):   # the chunk kernel's arithmetic: fp64 sum of squares per chunk slot
+            norm.launched[bi] = True
+            c0, c1, _ = norm.buckets[bi]
+            for c in range(c0, c1):
+                b, e = chunks[c]
+                opt._chunk_sq[c] = (st.grad[b:e].double() ** 2).sum()
+                hits.append(c)
+        norm._launch = fake_launch
+        for window in range(2):
+            for micro in range(2):
+                update = micro == 1
+                red.arm(update)
+                norm.arm(update)
+                for i, (n, *_) in enumerate(specs):
+                    v = float(rank + 1 + i % 8 + 10 * micro + 20 * window)
+                    g = st.params[n].grad
+                    g.fill_(v) if micro == 0 else g.add_(v)
+                for n in reversed(st.order):
+                    st.mark_ready([n])
+                if not update:
+                    assert not hits, "a GA micro-step summed norm chunks"
+            red.finish()
+            norm.finish()
+            assert sorted(hits) == list(range(len(chunks))), "every chunk exactly once"
+            hits.clear()
+            assert norm.take()
+            want = torch.tensor([(st.grad[b:e].double() ** 2).sum().item() for b, e in chunks], dtype=torch.float64)
+            assert torch.equal(opt._chunk_sq[:len(chunks)], want)   # sums of the all-reduced gradients
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _chunk_table(opt):
+    from onetrainer_amd import _lib
+    arr = (_lib.NormChunk * opt._n_chunks).from_buffer_copy(opt._chunks.cpu().numpy().tobytes())
+    return [(c.begin, c.end, c.tensor) for c in arr]
+
+
+def test_overlapped_norm_follows_the_reduce_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_norm, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res
+
+
 def test_bucket_partition_is_contiguous_and_complete():
     st = FlatParamStore(SPECS, torch.bfloat16, "cpu")
     if not dist.is_available():

@@ -37,7 +37,7 @@ def _port():
     return p
 
 
-def _run(tmp, world, fp32=False, global_batch=2, ga=1):
+def _run(tmp, world, fp32=False, global_batch=2, ga=1, norm_overlap=True):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -48,9 +48,9 @@ def _run(tmp, world, fp32=False, global_batch=2, ga=1):
         if world > 1:
             e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                      MASTER_PORT=str(port), OTAMD_DIST_BACKEND="gloo")
-        out = tmp / f"w{world}_{int(fp32)}_{global_batch}_{ga}_r{r}.pt"
+        out = tmp / f"w{world}_{int(fp32)}_{global_batch}_{ga}_{int(norm_overlap)}_r{r}.pt"
         cmd = [sys.executable, str(WORKER), "--global-batch", str(global_batch), "--out", str(out), "--ga", str(ga),
-               "--steps", str(ga)] + (["--fp32-reduce"] if fp32 else [])
+               "--steps", str(ga)] + (["--fp32-reduce"] if fp32 else []) + ([] if norm_overlap else ["--no-norm-overlap"])
         procs.append(subprocess.Popen(cmd, env=e))
         outs.append(out)
     for p in procs:
@@ -97,6 +97,19 @@ def test_dp4_ga2_bf16_vs_fp32_reduce(tmp_path):
     print(f"dp4 reduction error vs world 1: bf16 {rel_bf16:.3e}, fp32 staging {rel_fp32:.3e}")
 
 
+@pytest.mark.parametrize("fp32", [False, True])
+def test_dp2_overlapped_norm_equals_end_of_step(tmp_path, fp32):
+    """under data parallel the clip norm's squared sums run per bucket on the reducer's post stream as each all-reduce
+    completes (trainer/ddp.py reduced_hooks, OverlappedGradNorm(reducer=...)); the coefficient and the step must be
+    the end-of-step pass's bit for bit (same chunks, same fixed summation order), GA 2 included"""
+    for ga in (1, 2):
+        on = _run(tmp_path, 2, fp32, global_batch=2 * ga, ga=ga)
+        off = _run(tmp_path, 2, fp32, global_batch=2 * ga, ga=ga, norm_overlap=False)
+        for a, b in zip(on, off):
+            assert torch.equal(a["norm"], b["norm"]), (a["norm"], b["norm"])
+            assert torch.equal(a["grad"], b["grad"]) and torch.equal(a["param"], b["param"])
+
+
 def test_rccl_reducer_world1(tmp_path):
     """RCCL itself (torch.distributed 'nccl') under the bucketed reducer: a one-rank group on the box's GPU, the
     all-reduces issued from inside backward on the issue stream; a one-rank sum is the identity, so the step must
@@ -113,3 +126,4 @@ def test_rccl_reducer_world1(tmp_path):
     assert r["buckets"] > 3 and r["nonzero"]
     assert r["grad_equal"] and r["param_equal"], r
     assert r["grad_equal_fp32"] and r["param_equal_fp32"], r
+    assert r["norm_overlap_equal"], r

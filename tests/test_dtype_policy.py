@@ -60,9 +60,14 @@ def _outcome(c):
 
 
 def test_pinned_outcomes():
-    # TrainConfig.default_values(): SD 1.5 full fine-tune with fp32 master weights -> refused (not built)
-    assert _outcome(case("default_values")) == "refused"
-    assert _outcome(case("sd15")) == "refused"                      # C1's preset as it stands: fp32 weights
+    # TrainConfig.default_values() and C1's preset as it stands: SD 1.5 full fine-tune with fp32 master weights and a
+    # FLOAT_16 train dtype -> fp32 masters (round 6), bf16 compute, no GradScaler, fp32 norm gradients rounded: recorded
+    master = ["grad_scaler", "norm gradients", "train_dtype"]
+    assert _outcome(case("default_values")) == master
+    assert _outcome(case("sd15")) == master
+    assert _outcome(case("sd15", train_dtype="BFLOAT_16")) == ["norm gradients"]
+    assert dtype_plan(stand_in(case("sd15"))).master and dtype_plan(stand_in(case("sd15"))).network == "FLOAT_32"
+    assert _outcome(case("sd15", train_dtype="FLOAT_32")) == "refused"   # fp32 compute is not built
     assert _outcome(case("sd15", train_dtype="BFLOAT_16", weight_dtype="BFLOAT_16")) == []   # C2
     # #sdxl 1.0.json: bf16 weights, train_dtype left at FLOAT_16 -> bf16 compute, recorded
     assert _outcome(case("sdxl")) == ["train_dtype"]
@@ -85,9 +90,13 @@ def test_overrides_name_the_reference_values(i):
     except ValueError as e:
         fine_tune = c["fields"]["training_method"] == "FINE_TUNE"
         net = c["resolved"]["prior" if c["fields"]["model_type"].startswith("FLUX") else "unet"]
-        assert c["reference"]["compute"] == "FLOAT_32" or (fine_tune and net == "FLOAT_32"), (c, e)
+        assert c["reference"]["compute"] == "FLOAT_32", (c, e)
         return
-    assert plan.compute == "BFLOAT_16" and plan.network == "BFLOAT_16"
+    fine_tune = c["fields"]["training_method"] == "FINE_TUNE"
+    net = c["resolved"]["prior" if c["fields"]["model_type"].startswith("FLUX") else "unet"]
+    assert plan.compute == "BFLOAT_16"
+    assert plan.master == (fine_tune and net == "FLOAT_32")
+    assert plan.network == ("FLOAT_32" if plan.master else "BFLOAT_16")
     for o in plan.overrides:
         if o["field"] == "train_dtype":
             assert o["reference"] == c["reference"]["compute"]
@@ -102,8 +111,35 @@ def test_overrides_name_the_reference_values(i):
 
 def test_create_model_refuses_before_allocating():
     from onetrainer_amd.util import create
-    with pytest.raises(ValueError, match="fp32 master weights"):
-        create.create_model(stand_in(case("default_values")), "meta")
+    with pytest.raises(ValueError, match="fp32 compute is not built"):
+        create.create_model(stand_in(case("default_values", train_dtype="FLOAT_32")), "meta")
+
+
+def test_fp32_master_store():
+    """the reference's default (FLOAT_32 weights, full fine-tune): fp32 masters hold the trained values, the bf16
+    working copy is their round-to-nearest cast (autocast's), the state dict / savers read the masters"""
+    import torch
+
+    from onetrainer_amd.module import unet as U
+    from onetrainer_amd.util import create
+    m = create.create_model(stand_in(case("default_values")), "cpu", seed=3, unet_config=U.tiny_sd15_config())
+    st = m.unet.store
+    assert st.master is not None and st.master.dtype == torch.float32 and st.data.dtype == torch.bfloat16
+    assert st.grad.dtype == torch.bfloat16
+    assert torch.equal(st.data, st.master.to(torch.bfloat16))
+    sd = m.unet.state_dict()
+    assert all(v.dtype == torch.float32 for v in sd.values())
+    assert any(not torch.equal(v, v.bfloat16().float()) for v in sd.values())   # fp32 values, not bf16 ones
+    # load -> fp32 master exactly, bf16 working copy re-cast
+    m2 = create.create_model(stand_in(case("default_values")), "cpu", seed=9, unet_config=U.tiny_sd15_config())
+    m2.unet.load_state_dict(sd)
+    assert torch.equal(m2.unet.store.master, st.master) and torch.equal(m2.unet.store.data, st.data)
+    # a bf16 network keeps no master copy and loads the same values as their bf16 cast
+    m3 = create.create_model(stand_in(case("default_values", weight_dtype="BFLOAT_16")), "cpu", seed=9,
+                             unet_config=U.tiny_sd15_config())
+    assert m3.unet.store.master is None
+    m3.unet.load_state_dict(sd)
+    assert torch.equal(m3.unet.store.data, st.data)
 
 
 def test_train_script_starts_from_the_reference_defaults(tmp_path):
@@ -119,9 +155,9 @@ def test_train_script_starts_from_the_reference_defaults(tmp_path):
     cfg = mod.load_config(str(p))
     assert cfg.train_dtype == "FLOAT_16"
     assert [o["field"] for o in dtype_plan(cfg).overrides] == ["train_dtype"]
-    p.write_text(json.dumps({"model_type": "STABLE_DIFFUSION_15"}))
-    with pytest.raises(ValueError):
-        dtype_plan(mod.load_config(str(p)))
+    p.write_text(json.dumps({"model_type": "STABLE_DIFFUSION_15"}))   # the reference's defaults: fp32 weights
+    plan = dtype_plan(mod.load_config(str(p)))
+    assert plan.master and [o["field"] for o in plan.overrides] == ["train_dtype", "norm gradients", "grad_scaler"]
 
 
 @pytest.mark.skipif(not REF.exists(), reason="reference checkout only in the build container")

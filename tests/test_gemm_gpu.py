@@ -191,103 +191,3 @@ def test_every_tile_explicit(dev, tile, monkeypatch):
         refw = torch.nn.grad.conv2d_weight(nchw(xc), (96, 64, 3, 3), nchw(yc), padding=1)
         close(dwc, refw.permute(0, 2, 3, 1), tol=2e-2)
         close(dbc, yc.float().sum((0, 1, 2)), tol=2e-3)
-
-
-
-
-@pytest.mark.parametrize("tile", [0, 1, 2, 4, 7, 8])
-def test_half_k_schedule_matches(dev, tile, monkeypatch):
-    """gemm2h_kernel (half-K DMA units, otamd_gemm_set_schedule(1)) against the default schedule bit for bit, and
-    against an exact integer reference, for every operand mode pair the plain forms use, with tile tails, split-K,
-    the fused bias gradient (column sums) and a 3x3 conv weight gradient"""
-    from onetrainer_amd import _lib
-    lib = _lib.lib()
-    torch.manual_seed(tile)
-    M, N, Kd = 300, 200, 200
-    x = torch.randint(-3, 4, (M, Kd), device=dev).to(BF)
-    w = torch.randint(-3, 4, (N, Kd), device=dev).to(BF)
-    dy = torch.randint(-2, 3, (M, N), device=dev).to(BF)
-    conv_x = torch.randint(-2, 3, (2, 12, 10, 64), device=dev).to(BF)
-    conv_dy = torch.randint(-2, 3, (2, 12, 10, 96), device=dev).to(BF)
-
-    def run():
-        outs = []
-        for splits in (1, 2):
-            monkeypatch.setenv("OTAMD_GEMM_PLAN", ";".join(f"{a},{b},{m},{n},{k}:{tile}:{splits}" for a, b, m, n, k in
-                                                          ((0, 0, M, N, Kd), (0, 1, M, Kd, N), (1, 1, N, Kd, M),
-                                                           (1, 4, 96, 9 * 64, 240))))
-            K._PLAN_OVERRIDES = None
-            y = K.linear(x, w, out_dtype=torch.float32)
-            dx = K.linear_dgrad(dy, w, out=torch.empty(M, Kd, device=dev, dtype=torch.float32))
-            bg = torch.empty(N, device=dev, dtype=torch.float32)
-            dw = K.linear_wgrad(dy, x, out=torch.empty(N, Kd, device=dev, dtype=torch.float32), bias_grad=bg)
-            cb = torch.empty(96, device=dev, dtype=torch.float32)
-            cw = K.conv2d_wgrad(conv_dy, conv_x, 3, 1, 1, out=torch.empty(96, 3, 3, 64, device=dev, dtype=torch.float32),
-                                bias_grad=cb)
-            outs += [y, dx, dw, bg, cw, cb]
-        return outs
-
-    prev = lib.otamd_gemm_set_schedule(0)
-    try:
-        base = run()
-        lib.otamd_gemm_set_schedule(1)
-        hk = run()
-    finally:
-        lib.otamd_gemm_set_schedule(prev)
-        K._PLAN_OVERRIDES = None
-    for a, b in zip(base, hk):
-        assert torch.equal(a, b)
-    assert torch.equal(hk[0], x.float() @ w.float().t())
-    assert torch.equal(hk[1], dy.float() @ w.float())
-    assert torch.equal(hk[2], dy.float().t() @ x.float()) and torch.equal(hk[3], dy.float().sum(0))
-    ref = torch.nn.grad.conv2d_weight(conv_x.permute(0, 3, 1, 2).float(), (96, 64, 3, 3),
-                                      conv_dy.permute(0, 3, 1, 2).float(), padding=1)
-    assert torch.equal(hk[4], ref.permute(0, 2, 3, 1)) and torch.equal(hk[5], conv_dy.float().sum((0, 1, 2)))
-
-
-@pytest.mark.parametrize("tile", [0, 4, 5, 6, 7])
-def test_splitk_fixup_matches_reduce_launch(dev, tile, monkeypatch):
-    """the in-launch split-K combine (splitk_fixup: last-arriving workgroup per tile sums the slabs) against the
-    separate reduce launch, bit for bit on random bf16 operands, across split counts, tile tails, every epilogue
-    operand (bias, residual, fp32 accumulate), the LoRA second K segment and conv forms; each configuration runs
-    twice so a counter left non-zero by a launch would show up in the next"""
-    from onetrainer_amd import _lib
-    lib = _lib.lib()
-    g = torch.Generator(device=dev).manual_seed(100 + tile)
-    M, N, Kd, r = 300, 200, 640, 64
-    rn = lambda *s: torch.randn(*s, device=dev, generator=g).to(BF)   # noqa: E731
-    x, w, dy, b, res = rn(M, Kd), rn(N, Kd) * 0.1, rn(M, N), rn(N), rn(M, N)
-    t, up = rn(M, r), rn(N, r) * 0.1
-    acc0 = torch.randn(M, N, device=dev, generator=g)
-    cx, cw, crow = rn(2, 12, 10, 64), rn(96, 3, 3, 64) * 0.1, rn(2, 96)
-
-    def run():
-        outs = []
-        for splits in (2, 3, 5):
-            monkeypatch.setenv("OTAMD_GEMM_PLAN", ";".join(f"{a},{b_},{m},{n},{k}:{tile}:{splits}" for a, b_, m, n, k in
-                                                          ((0, 0, M, N, Kd), (0, 1, M, Kd, N), (1, 1, N, Kd, M),
-                                                           (0, 0, M, N, Kd + r), (2, 0, 240, 96, 576))))
-            K._PLAN_OVERRIDES = None
-            for _ in range(2):
-                outs.append(K.linear(x, w, bias=b, residual=res))
-                a32 = acc0.clone()
-                outs.append(K.linear(x, w, out=a32, accumulate=True))
-                outs.append(K.linear_dgrad(dy, w))
-                outs.append(K.linear_wgrad(dy, x, alpha=0.5))
-                outs.append(K.linear(x, w, lora=(t, up)))
-                outs.append(K.conv2d(cx, cw, stride=1, pad=1, rowvec=crow))
-        return outs
-
-    prev = lib.otamd_gemm_set_fixup_limit(0)
-    try:
-        base = run()
-        lib.otamd_gemm_set_fixup_limit(1 << 40)
-        fix = run()
-    finally:
-        lib.otamd_gemm_set_fixup_limit(-1)
-        K._PLAN_OVERRIDES = None
-    assert prev == 0   # off by default (DESIGN.md §3, round 5)
-    for i, (a, b_) in enumerate(zip(base, fix)):
-        assert torch.equal(a, b_), (i, (a.float() - b_.float()).abs().max().item())
-    ref = (x.float() @ w.float().t() + b.float() + res.float())
-    assert (base[0].float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()

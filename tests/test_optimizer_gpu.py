@@ -71,6 +71,48 @@ def test_fused_adamw_f32(dev):
             np.testing.assert_allclose(st.params[n].detach().cpu().numpy().reshape(-1), p, rtol=0, atol=1e-8)
 
 
+@pytest.mark.parametrize("clip", [False, True])
+def test_fused_adamw_master_bitexact(dev, clip):
+    """fp32 master weights (weight_dtype FLOAT_32 full fine-tune): fp32 p / m / v and the bf16 working copy against
+    oracle.adamw.adamw_step_master bit for bit over 3 steps, with the fp32 clip (norms and coefficient in fp32 from bf16
+    gradients) against oracle.adamw.clip_grad_norm_f32"""
+    torch.manual_seed(2)
+    st = FlatParamStore([(n, s, "g") for n, s in SHAPES], torch.bfloat16, dev, master=True)
+    for n, s in SHAPES:
+        st.write(n, torch.randn(s) * 0.05)
+    assert torch.equal(st.data, st.master.to(torch.bfloat16))
+    opt = FusedAdamW(st, [{"params": [st.params[n] for n, _ in SHAPES]}], lr=3e-4, weight_decay=1e-2, seed=5)
+    assert opt.exp_avg.dtype == torch.float32
+    ref = {n: (st.value(n).cpu().numpy().reshape(-1).copy(), np.zeros(np.prod(s), np.float32),
+               np.zeros(np.prod(s), np.float32)) for n, s in SHAPES}
+    for step in range(1, 4):
+        for n, s in SHAPES:
+            st.params[n].grad.copy_(torch.randn(s) * 10 ** (-2 + step) * (3 if clip else 1))
+        coef = None
+        if clip:
+            total = opt.clip_grad_norm_(1.0).item()
+            gl = [OA.bf16_to_f32(bits(st.params[n].grad).reshape(-1)) for n, _ in SHAPES]
+            tot_ref, coef_ref = OA.clip_grad_norm_f32(gl, 1.0)
+            assert abs(total - tot_ref) <= 1e-6 * tot_ref
+            coef = np.float32(opt.clip_out[0].item())   # the device coefficient (its fp32 sum order) drives both
+            assert abs(coef - coef_ref) <= 1e-6 * coef_ref
+        seed_before = opt.seed
+        opt.step()
+        assert opt.seed == seed_before   # no stochastic rounding on fp32 parameters (adamw_extensions.py:144)
+        for n, s in SHAPES:
+            p, m, v = ref[n]
+            slot = st.slots[n]
+            sl = slice(slot.offset, slot.offset + slot.numel)
+            p, m, v, w = OA.adamw_step_master(p, bits(st.params[n].grad).reshape(-1), m, v, step, 3e-4, clip_coef=coef)
+            ref[n] = (p, m, v)
+            assert np.array_equal(opt.exp_avg[sl].cpu().numpy(), m), (n, step, "m")
+            assert np.array_equal(opt.exp_avg_sq[sl].cpu().numpy(), v), (n, step, "v")
+            assert np.array_equal(st.value(n).cpu().numpy().reshape(-1), p), (n, step, "p")
+            assert np.array_equal(bits(st.params[n]).reshape(-1), w), (n, step, "working copy")
+    sd = opt.state_dict()
+    assert sd["state"][0]["exp_avg"].dtype == torch.float32
+
+
 def test_state_dict_roundtrip(dev):
     st = FlatParamStore([(n, s, "g") for n, s in SHAPES], torch.bfloat16, dev)
     opt = FusedAdamW(st, [{"params": [st.params[n] for n, _ in SHAPES]}], lr=1e-3)

@@ -13,7 +13,7 @@ from onetrainer_amd.util.config.TrainConfig import TrainConfig
 from oracle import diffusion as OD
 from oracle import unet as OU
 
-from _oracle_opt import OracleBF16AdamW
+from _oracle_opt import OracleBF16AdamW, OracleMasterAdamW
 
 pytestmark = pytest.mark.gpu
 
@@ -84,12 +84,15 @@ def test_train_step_matches_oracle(dev, ptype):
     assert min(cos) > 0.999, cos
 
 
-def test_sd15_train_step_matches_oracle(dev):
+@pytest.mark.parametrize("weight_dtype", ["BFLOAT_16", "FLOAT_32"])
+def test_sd15_train_step_matches_oracle(dev, weight_dtype):
     """SD 1.5 plugin (BaseStableDiffusionSetup.py:135-330): one text encoder, no add-embedding,
-    80-wide (flash) and 160-wide (materialized) heads."""
+    80-wide (flash) and 160-wide (materialized) heads.  FLOAT_32: the reference's default weight dtype (C1's preset),
+    fp32 master weights behind the bf16 working copy (util/dtype_util.py), against the fp32 oracle optimizer."""
     torch.manual_seed(0)
     ucfg = U.tiny_sd15_config()
     cfg = TrainConfig.default_values()
+    cfg.weight_dtype = weight_dtype
     cfg.model_type = "STABLE_DIFFUSION_15"
     cfg.batch_size = 2
     cfg.learning_rate = 1e-4
@@ -104,7 +107,9 @@ def test_sd15_train_step_matches_oracle(dev):
     assert type(tr.model_setup).__name__ == "StableDiffusionFineTuneSetup"
     res = 128
     batch = synthetic_sdxl_batch(2, res, res, dev, seed=1, te1_dim=96, sdxl=False, scaling_factor=0.18215)
-    opt = OracleBF16AdamW(om.parameters(), lr=1e-4, weight_decay=1e-2)
+    master = weight_dtype == "FLOAT_32"
+    assert (model.unet.store.master is not None) == master
+    opt = (OracleMasterAdamW if master else OracleBF16AdamW)(om.parameters(), lr=1e-4, weight_decay=1e-2)
     betas = OD.scaled_linear_betas()
     lat = batch["latent_image"].cpu().float()
     ehs = batch["text_encoder_hidden_state"].float().cpu()
@@ -122,9 +127,16 @@ def test_sd15_train_step_matches_oracle(dev):
         loss.backward()
         opt.step()
         ref.append(loss.item())
-    print("sd15 losses hip", ours, "oracle", ref)
+    print("sd15", weight_dtype, "losses hip", ours, "oracle", ref)
     for a, b in zip(ours, ref):
         assert abs(a - b) <= 1e-3 * abs(b), (ours, ref)
+    if master:   # the masters carry the update below bf16 resolution; the working copy is their rne cast
+        st = model.unet.store
+        assert torch.equal(st.data, st.master.to(torch.bfloat16))
+        assert not torch.equal(st.master, st.data.float())
+        for k, v in model.unet.state_dict().items():   # the trained masters against the oracle's fp32 weights
+            o = dict(om.named_parameters())[k].detach()
+            assert torch.allclose(v.cpu(), o, rtol=0, atol=1e-3), k   # 2 steps of <= ~2 lr each
 
 
 def test_dp_noise_slices_match_global(dev):

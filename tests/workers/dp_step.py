@@ -25,7 +25,10 @@ def main():
     ap.add_argument("--fp32-reduce", action="store_true")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--ga", type=int, default=1, help="gradient accumulation steps (run --steps = ga for one update)")
+    ap.add_argument("--no-norm-overlap", action="store_true", help="clip norm after the step instead of per bucket")
     args = ap.parse_args()
+    if args.no_norm_overlap:
+        os.environ["OTAMD_NORM_OVERLAP"] = "0"
     import torch
 
     from onetrainer_amd.dataLoader.SyntheticDataLoader import synthetic_sdxl_batch
@@ -51,6 +54,9 @@ def main():
     tr = GenericTrainer(cfg, model=model)
     tr.start()
     assert tr.world == world and tr.rank == rank
+    overlap = model.optimizer.norm_overlap is not None
+    assert overlap == (not args.no_norm_overlap), overlap
+    assert not overlap or model.optimizer.norm_overlap.dp == (world > 1)
     full = synthetic_sdxl_batch(args.global_batch, args.res, args.res, dev, seed=1, te1_dim=48, te2_dim=48,
                                 pooled_dim=64)
     mine = {}
@@ -68,7 +74,7 @@ def main():
     torch.cuda.synchronize()
     st = model.train_store
     torch.save({"loss": torch.stack(losses), "norm": torch.stack(norms), "grad": st.grad.float().cpu(),
-                "param": st.data.cpu(), "world": world, "rank": rank}, args.out)
+                "param": st.data.cpu(), "world": world, "rank": rank, "norm_overlap": overlap}, args.out)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -36,7 +36,7 @@ def main():
     dist.init_process_group("nccl", rank=0, world_size=1, timeout=datetime.timedelta(seconds=120))
     assert dist.get_backend() == "nccl"
 
-    def run(reducer_kind):
+    def run(reducer_kind, norm_overlap=False):
         cfg = TrainConfig.default_values()
         cfg.batch_size = 2
         cfg.learning_rate = 1e-4
@@ -49,18 +49,23 @@ def main():
         if reducer_kind is not None:
             tr.reducer = GradBucketReducer(model.train_store, bucket_bytes=1 << 20, reduce_fp32=reducer_kind == "fp32")
             nb = len(tr.reducer.buckets)
+            if norm_overlap:   # the clip norm's sums per bucket on the reducer's post stream, after each RCCL reduce
+                from onetrainer_amd.util.optimizer.adamw_fused import OverlappedGradNorm
+                model.optimizer.norm_overlap = OverlappedGradNorm(model.optimizer, reducer=tr.reducer)
         batch = synthetic_sdxl_batch(2, 128, 128, dev, seed=1, te1_dim=48, te2_dim=48, pooled_dim=64)
         for _ in range(2):
             tr.train_step(batch)
         torch.cuda.synchronize()
         st = model.train_store
-        return st.grad.float().cpu(), st.data.cpu(), nb
+        return st.grad.float().cpu(), st.data.cpu(), nb, model.optimizer.clip_out.cpu()
 
-    g0, p0, _ = run(None)
-    g1, p1, nb = run("bf16")
-    g2, p2, _ = run("fp32")
+    g0, p0, _, c0 = run(None)
+    g1, p1, nb, _ = run("bf16")
+    g2, p2, _, _ = run("fp32")
+    g3, p3, _, c3 = run("bf16", norm_overlap=True)
     torch.save({"grad_equal": bool(torch.equal(g0, g1)), "param_equal": bool(torch.equal(p0, p1)),
                 "grad_equal_fp32": bool(torch.equal(g0, g2)), "param_equal_fp32": bool(torch.equal(p0, p2)),
+                "norm_overlap_equal": bool(torch.equal(g0, g3) and torch.equal(p0, p3) and torch.equal(c0, c3)),
                 "buckets": nb, "nonzero": bool(g0.abs().sum() > 0)}, args.out)
     dist.destroy_process_group()
 

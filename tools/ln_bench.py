@@ -58,7 +58,6 @@ def main():
                 "param_grad": (lambda: K.layernorm_param_grad(x, dy, stats, dg, db), 2 * E),
                 "bwd_res+param": (lambda: (K.layernorm_bwd_res(x, dy, dres, gamma, stats),
                                            K.layernorm_param_grad(x, dy, stats, dg, db)), 4 * E),
-                "bwd_fused": (lambda: K.layernorm_bwd_fused(x, dy, gamma, stats, dg, db, dres=dres), 4 * E),
             }
             for name, (fn, nbytes) in cases.items():
                 fn()
