@@ -386,6 +386,16 @@ __global__ void clip_coef_kernel(const double* __restrict__ tensor_sq, int n_ten
 }
 
 // ---- C ABI ----------------------------------------------------------------------
+// workgroup cap of the update launches: OTAMD_ADAMW_BLOCKS (default: the whole chip).  An update overlapped with
+// the next forward on its own stream (util/optimizer/adamw_fused.py) holds only that many CUs' worth of slots.
+static long long adamw_max_blocks(long long dflt) {
+  static const long long cap = [] {
+    const char* e = getenv("OTAMD_ADAMW_BLOCKS");
+    return e ? atoll(e) : 0LL;
+  }();
+  return cap > 0 ? std::min(cap, dflt) : dflt;
+}
+
 static int adamw_grid(long long nvec) {
   long long blocks = (nvec + 255) / 256;
   if (blocks > 256 * 16) blocks = 256 * 16;
@@ -417,7 +427,7 @@ OTAMD_API int otamd_adamw_bf16_range(void* p, const void* g, void* m, void* v, l
   if (const char* e = getenv("OTAMD_ADAMW_LUT")) { lut = shared && e[0] != '0'; nt = e[0] != '1'; }
   const long long v0 = begin / 8, v1 = end / 8;
   if (lut) {
-    const int blocks = (int)std::max(1LL, std::min<long long>((v1 - v0 + 1023) / 1024, 512));
+    const int blocks = (int)std::max(1LL, std::min<long long>((v1 - v0 + 1023) / 1024, adamw_max_blocks(512)));
     if (nt)
       adamw_bf16_lut_kernel<true><<<blocks, 1024, 0, stream>>>((bf16_t*)p, (const bf16_t*)g, (bf16_t*)m, (bf16_t*)v, v0,
                                                                v1, G, clip_coef, stochastic_rounding, seed);
@@ -467,7 +477,7 @@ OTAMD_API int otamd_adamw_master_range(void* p32, const void* g16, void* m32, vo
   for (int i = 0; i < n_groups; ++i) G.g[i] = groups[i];
   G.n = n_groups;
   const long long v0 = begin / 8, v1 = end / 8;
-  const int blocks = (int)std::max(1LL, std::min<long long>((v1 - v0 + 255) / 256, 256 * 16));
+  const int blocks = (int)std::max(1LL, std::min<long long>((v1 - v0 + 255) / 256, adamw_max_blocks(256 * 16)));
   adamw_master_kernel<<<blocks, 256, 0, stream>>>((float*)p32, (const bf16_t*)g16, (float*)m32, (float*)v32,
                                                   (bf16_t*)w16, v0, v1, G, clip_coef);
   OTAMD_CHECK_LAUNCH();

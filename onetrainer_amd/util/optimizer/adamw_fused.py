@@ -83,14 +83,18 @@ class FusedAdamW(torch.optim.Optimizer):
                         and self.master is None and os.environ.get("OTAMD_OPT_OVERLAP", "0") == "1")
         self._opt_chunks = []
         if self.overlap:
-            target = store.numel // 16
-            b = 0
+            # chunk ends at 1/256, 1/128, ..., 1/16 of the store, then every 1/16 (tensor boundaries): the forward's first
+            # layers wait only for a small first chunk, the rest of the update runs beside them
+            ends = [store.numel >> k for k in range(8, 4, -1)] + [store.numel * i // 16 for i in range(1, 17)]
+            b, t = 0, 0
             for n in store.order:
                 s = store.slots[n]
                 e = (s.offset + s.numel + 7) // 8 * 8
-                if e - b >= target:
+                if t < len(ends) and e >= ends[t]:
                     self._opt_chunks.append((b, e))
                     b = e
+                    while t < len(ends) and ends[t] <= e:
+                        t += 1
             if b < store.numel:
                 self._opt_chunks.append((b, store.numel))
             self._stream = torch.cuda.Stream(device=store.device)

@@ -97,6 +97,16 @@ def test_dp4_ga2_bf16_vs_fp32_reduce(tmp_path):
     print(f"dp4 reduction error vs world 1: bf16 {rel_bf16:.3e}, fp32 staging {rel_fp32:.3e}")
 
 
+def test_dp8_bf16_vs_fp32_reduce(tmp_path):
+    """eight ranks at b=1 (the node's rank count; gloo on the one GPU) against one rank at global batch 8: at world 8 the
+    bf16 in-place ring sum rounds up to 7 times per element, the fp32 staging (dp_reduce_fp32) once -- both held to
+    the same bounds as world 2 / 4, the two errors printed side by side"""
+    ref = _run(tmp_path, 1, global_batch=8)[0]
+    rel_bf16 = _compare(_run(tmp_path, 8, False, global_batch=8), ref, False, "dp8 vs dp1")
+    rel_fp32 = _compare(_run(tmp_path, 8, True, global_batch=8), ref, True, "dp8 vs dp1")
+    print(f"dp8 reduction error vs world 1: bf16 {rel_bf16:.3e}, fp32 staging {rel_fp32:.3e}")
+
+
 @pytest.mark.parametrize("fp32", [False, True])
 def test_dp2_overlapped_norm_equals_end_of_step(tmp_path, fp32):
     """under data parallel the clip norm's squared sums run per bucket on the reducer's post stream as each all-reduce
