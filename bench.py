@@ -417,6 +417,7 @@ def main():
                    "model": mname, "global_batch": args.batch * world,
                    "seq_len": (args.res // 8) ** 2, "parallelism": f"dp{world}"},
         "loss": round(loss_val, 5),
+        "lora_forwards_fused_vs_two_launch": list(K.lora_fused_counts()),
         "roofline": {"bound": "mfma", "achieved": round(g_achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(g_achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": (pmc["gemm_total_gb"] if pmc and default_shape else None),

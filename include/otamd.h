@@ -60,6 +60,15 @@ typedef struct GemmArgs {
      GEMM slabs (splits * M floats) and the split-K reduce folds them */
   void* colsum; int colsum_f32; int colsum_acc;
   float* colsum_slab;
+  /* optional LoRA down-projection fused into a forward base GEMM (linear or 3x3 conv, B = K-mode weights, split 1,
+     tiles 1 / 4 / 7 / 8, lora_r = 32): t = A D^T over the K loop for the adapter part of the tile's columns,
+     rounded to bf16, stored to T [M][ldt] by the part's first tile column, and t (B2)^T added as the second K
+     segment -- replaces the separate down GEMM x A^T + its split-K reduce before the fused up projection
+     (LoRAModule.forward, modules/module/LoRAModule.py:318-322).  D = down [P*lora_r][K], B2 / ldb2 = up [N][P*lora_r],
+     lora_pw = output columns per part; K = the base K, A2 = NULL.  D == NULL: off. */
+  const void* D; long long ldd;
+  void* T; long long ldt;
+  int lora_r, lora_pw;
 } GemmArgs;
 
 typedef struct AttnArgs {

@@ -34,7 +34,9 @@ class GemmArgs(C.Structure):
                 ("K1", C.c_int), ("K2", C.c_int),
                 ("batch", C.c_int), ("bdiv", C.c_int), ("sa0", C.c_longlong), ("sa1", C.c_longlong),
                 ("sb0", C.c_longlong), ("sb1", C.c_longlong), ("sc0", C.c_longlong), ("sc1", C.c_longlong),
-                ("colsum", C.c_void_p), ("colsum_f32", C.c_int), ("colsum_acc", C.c_int), ("colsum_slab", C.c_void_p)]
+                ("colsum", C.c_void_p), ("colsum_f32", C.c_int), ("colsum_acc", C.c_int), ("colsum_slab", C.c_void_p),
+                ("D", C.c_void_p), ("ldd", C.c_longlong), ("T", C.c_void_p), ("ldt", C.c_longlong),
+                ("lora_r", C.c_int), ("lora_pw", C.c_int)]
 
 
 class AdamwGroup(C.Structure):

@@ -45,6 +45,13 @@ struct GemmArgs {
   // split-K reduce.  v2 tiles only; tile-column 0 workgroups accumulate them from the LDS image of A.
   void* colsum; int colsum_f32; int colsum_acc;
   float* colsum_slab;
+  // LoRA down-projection fused into the K loop of a forward base GEMM (v2 tiles, gemm2_tiles_e.hip): D = down
+  // [P*lora_r][K] (K-mode, the K layout of B), B2 / ldb2 = up [N][P*lora_r] (alpha/rank folded in), T = t [M][ldt]
+  // (bf16 out, for the backward), lora_pw = output columns per adapter part (tiles never straddle parts).  K is the
+  // base K (no second segment operand A2).  D == nullptr: off.
+  const bf16_t* D; long long ldd;
+  bf16_t* T; long long ldt;
+  int lora_r, lora_pw;
 };
 
 __device__ __forceinline__ void gemm_batch_offset(GemmArgs& a) {

@@ -603,7 +603,7 @@ OTAMD_API long long otamd_gemm_plan(const GemmArgs* in, int splits, int* splits_
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -1;
   int s = splits;
   if (in->batch > 1) s = 1;
-  if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT || in->A2 != nullptr).splits;
+  if (s <= 0) s = plan_gemm(in->M, in->N, in->K, 32, in->bmode == OPM_CONV_WT || in->A2 != nullptr || in->D != nullptr).splits;
   if (splits_out) *splits_out = s;
   return s > 1 ? otamd_gemm_ws_bytes(in, s) : 0;
 }
@@ -615,7 +615,7 @@ static int resolve_tile(const GemmArgs& a, int splits, GemmPlan plan, bool v2_on
 // 5 = 128x64, 6 = 64x128, 7 = 128x160, 8 = 256x160
 OTAMD_API int otamd_gemm_plan_tile(const GemmArgs* in, int splits) {
   if (!in || in->M <= 0 || in->N <= 0 || in->K <= 0) return -9;
-  const bool v2_only = in->bmode == OPM_CONV_WT || in->A2 != nullptr;
+  const bool v2_only = in->bmode == OPM_CONV_WT || in->A2 != nullptr || in->D != nullptr;
   GemmPlan plan = plan_gemm(in->M, in->N, in->K, splits > 0 ? splits : 32, v2_only);
   if (splits > 0) plan = plan_gemm(in->M, in->N, in->K, 1, v2_only), plan.splits = splits;
   const long long kps = ((long long)(in->K + plan.splits - 1) / plan.splits + BK - 1) / BK * BK;
@@ -647,7 +647,14 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   if (!in) return OTAMD_EINVAL;
   GemmArgs a = *in;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
-  const bool v2_only = a.bmode == OPM_CONV_WT || a.A2 != nullptr;
+  const bool v2_only = a.bmode == OPM_CONV_WT || a.A2 != nullptr || a.D != nullptr;
+  if (a.D) {   // LoRA down-projection fused into a forward base GEMM (gemm2_tiles_e.hip)
+    if (a.A2 || !a.B2 || !a.T || a.lora_r != 32 || a.lora_pw <= 0 || a.N % a.lora_pw || a.batch > 1 || a.colsum)
+      return OTAMD_EINVAL;
+    if (!((a.amode == OPM_K || a.amode == OPM_CONV_FWD) && a.bmode == OPM_K)) return OTAMD_EUNSUPPORTED;
+    if ((a.ldd % 8) || (a.ldb2 % 8) || (a.ldt % 8) || !aligned16(a.D) || !aligned16(a.B2) || !aligned16(a.T))
+      return OTAMD_EINVAL;
+  }
   if (a.A2) {   // second K segment (LoRA fusion): forms and alignment the v2 kernels support
     if (!a.B2 || a.K1 <= 0 || a.K2 <= 0 || a.K1 % 64 || a.K != a.K1 + a.K2) return OTAMD_EINVAL;
     if (!((a.amode == OPM_K || a.amode == OPM_CONV_FWD) && a.bmode == OPM_K) && !(a.amode == OPM_K && a.bmode == OPM_MN))
@@ -702,10 +709,11 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   if (a.colsum && (tile < 0 || tile == 3)) tile = 0;   // the fused column sums live in the 8-wave v2 kernels
   if (v2_only && tile < 0) return OTAMD_EUNSUPPORTED;
   int rc = OTAMD_EUNSUPPORTED;
+  if (a.D && splits != 1) return OTAMD_EUNSUPPORTED;   // t needs the whole K range in one workgroup
   if (tile >= 0) rc = gemm2_launch(a, tile, splits, stream);
   if (rc == OTAMD_ELAUNCH) return rc;
   if (rc != OTAMD_OK) {
-    if (!fn || a.A2 || a.colsum) return rc;   // v1 has no conv-weight B, no second K segment, no column sums
+    if (!fn || a.A2 || a.colsum || a.D) return rc;   // v1 has no conv-weight B, no second K segment, no column sums
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid(tiles, a.batch > 1 ? a.batch : 1, splits);
     hipLaunchKernelGGL(fn, grid, dim3(NTHREADS), 65536, stream, a);

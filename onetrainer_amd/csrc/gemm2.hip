@@ -10,6 +10,7 @@ gemm2_fn gemm2_pick_a(int tile, int am, int bm, bool seg2, bool cs);   // 0, 3  
 gemm2_fn gemm2_pick_b(int tile, int am, int bm, bool seg2, bool cs);   // 1, 2   256x128, 128x256
 gemm2_fn gemm2_pick_c(int tile, int am, int bm, bool seg2, bool cs);   // 4, 5, 6, 9, 10  128x128, 128x64, 64x128
 gemm2_fn gemm2_pick_d(int tile, int am, int bm, bool seg2, bool cs);   // 7, 8   x160
+gemm2_fn gemm2_pick_ld(int tile, int am, int bm, int ldr);              // 0, 1, 4, 7, 8 with the fused down-projection
 
 // byte extent an operand's gathers may touch (the DMA descriptor's range)
 static long long operand_bytes(int mode, const bf16_t* p, long long ld, int MN, int K, const ConvGeom& g) {
@@ -41,7 +42,10 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   // OTAMD_SKINNY_NS4=1: tiles 5 / 6 run on the 4-deep ring (tiles 9 / 10) when they have no second K segment
   static const bool skinny4 = [] { const char* e = getenv("OTAMD_SKINNY_NS4"); return e && e[0] == '1'; }();
   if (skinny4 && (tile == 5 || tile == 6) && !seg2) tile += 4;
-  switch (tile) {
+  if (a.D) {   // LoRA down-projection fused (forward forms; split 1, whole adapter parts per tile: checked here)
+    if (seg2 || cs || splits != 1 || a.batch > 1) return OTAMD_EUNSUPPORTED;
+    fn = gemm2_pick_ld(tile, a.amode, a.bmode, a.lora_r);
+  } else switch (tile) {
     case 0: case 3: fn = gemm2_pick_a(tile, a.amode, a.bmode, seg2, cs); break;
     case 1: case 2: fn = gemm2_pick_b(tile, a.amode, a.bmode, seg2, cs); break;
     case 4: case 5: case 6: case 9: case 10: fn = gemm2_pick_c(tile, a.amode, a.bmode, seg2, cs); break;
@@ -54,8 +58,9 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
                                  {64, 128, 8, 4}};
   if (tile >= 0 && tile < 11) { BMv = geo[tile][0]; BNv = geo[tile][1]; NWv = geo[tile][2]; NSv = geo[tile][3]; }
   if (!fn) return OTAMD_EUNSUPPORTED;
+  if (a.D && (a.lora_pw % BNv || a.N % a.lora_pw)) return OTAMD_EUNSUPPORTED;
   const int tiles = ((a.M + BMv - 1) / BMv) * ((a.N + BNv - 1) / BNv);
-  const int lds = NSv * (BMv + BNv) * 128 + (cs && BMv == 256 ? (NWv * 64 / (BMv / 8)) * BMv * 4 : 0);
+  const int lds = NSv * (BMv + BNv + (a.D ? a.lora_r : 0)) * 128 + (cs && BMv == 256 ? (NWv * 64 / (BMv / 8)) * BMv * 4 : 0);
   {   // the LDS opt-in once per kernel instance (a per-launch driver call costs host time on every GEMM)
     static std::mutex mu;
     static std::unordered_set<const void*> done;

@@ -232,24 +232,42 @@ __device__ __forceinline__ int mn_chunk_off(int k, int c) {   // 16-byte chunk c
   return k * RB + ((((c >> 1)) ^ mn_swz_rb<RB>(k)) << 5) + ((c & 1) << 4);
 }
 
-template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2, bool CS = false>
-__global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 || BN == 160)) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
+// LDR > 0: the LoRA down-projection of a frozen base GEMM computed inside its K loop (forward forms, B = K-mode
+// weights).  The tile's output columns lie in one adapter part p = n0 / lora_pw; the part's LDR down rows D[p*LDR ..]
+// ride in each stage as a third K-mode image, and every wave accumulates t = A D_p^T for all its rows and LDR / WN of
+// the part's columns beside the base MFMAs.  After the loop t is rounded to bf16 (as the separate t = x A^T GEMM
+// stores it), staged in LDS, written to T by the part's first tile column (for the adapter weight gradients), and
+// multiplied by the up projection U = B2 [N][P*LDR] (alpha/rank folded in) into the same accumulators: the second K
+// segment of the SEG2 form, without the t GEMM, its split-K reduce and their two launch boundaries.  The t sums run
+// over K in the same 64-deep steps and 16x16x32 MFMAs as a one-split t GEMM, so t, and y, are bit-identical to that
+// path.  LD tiles use 2 waves along N (wave tiles (BM / 4) x (BN / 2)), so each wave owns whole t column fragments.
+template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2, bool CS = false, int LDR = 0>
+__global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && (BN == 128 || BN == 160)) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
                                                                  unsigned a2_bytes, unsigned b2_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool LD = LDR > 0;
   // BN = 160 (N = 320 / 640 / 1280 in 2 / 4 / 8 tiles, no padding): waves 4 x 2, wave tile (BM/4) x 80
-  constexpr int WN = NW == 4 ? 2 : ((BM == 256 && BN == 128) || BN == 160 ? 2 : 4);
+  constexpr int WN = (NW == 4 || LD) ? 2 : ((BM == 256 && BN == 128) || BN == 160 ? 2 : 4);
   constexpr int WM = NW / WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MI = TM / 16, NJ = TN / 16;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
-  constexpr int STAGE = ABYTES + BBYTES;
-  constexpr int LOADS = Stage<AM, BM, NW>::NI + Stage<BMODE, BN, NW>::NI;
+  constexpr int RC = LDR / 16;               // t column fragments of the part
+  constexpr int RCW = LD ? RC / WN : 0;      // ... owned by one wave
+  constexpr int NBT = MI * RCW;              // 16 x 16 t blocks per wave
+  constexpr int TBYTES = LD ? LDR * 128 : 0;
+  static_assert(!LD || (!SEG2 && !CS && NS == 2 && NW == 8 && BMODE == OPM_K && RC % WN == 0 && RCW >= 1),
+                "down-projection fusion: forward forms, 8 waves, whole t fragments per wave");
+  constexpr int STAGE = ABYTES + BBYTES + TBYTES;
+  constexpr int NIT = LD ? Stage<OPM_K, LD ? LDR : 8, NW>::NI : 0;
+  constexpr int LOADS = Stage<AM, BM, NW>::NI + Stage<BMODE, BN, NW>::NI + NIT;
   // DMA pieces this wave issues per K-step (an image of NP pieces over NW waves: waves < NP % NW take one more)
   constexpr int NPA = Stage<AM, BM, NW>::NP, NPB = Stage<BMODE, BN, NW>::NP;
   static_assert(!SEG2 || NS == 2, "the LoRA second segment keeps the two-stage ring");
   constexpr bool AK = IsKMode<AM>::v, BKm = IsKMode<BMODE>::v;
   // per-wave DMA counts differ when an image does not split evenly: the prologue then drains fully
-  constexpr bool EVEN_LOADS = Stage<AM, BM, NW>::EVEN && Stage<BMODE, BN, NW>::EVEN && (!SEG2 || (Stage<OPM_K, BM, NW>::EVEN && Stage<BKm ? OPM_K : OPM_MN, BN, NW>::EVEN));
+  constexpr bool EVEN_LOADS = Stage<AM, BM, NW>::EVEN && Stage<BMODE, BN, NW>::EVEN && (!SEG2 || (Stage<OPM_K, BM, NW>::EVEN && Stage<BKm ? OPM_K : OPM_MN, BN, NW>::EVEN)) &&
+                              (!LD || Stage<OPM_K, LD ? LDR : 8, NW>::EVEN);
   if constexpr (!SEG2 && AM <= OPM_MN && BMODE <= OPM_MN) gemm_batch_offset(args);
 
   const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
@@ -281,11 +299,22 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     sa2.prepare(args.ga, args.lda2, m0, args.M, wave, lane);
     sb2.prepare(args.gb, args.ldb2, n0, args.N, wave, lane);
   }
+  // down-projection fusion: the part's LDR rows of D (K-mode, the K layout of B) as a third image per stage
+  const int lpart = LD ? n0 / args.lora_pw : 0;
+  Stage<OPM_K, LD ? LDR : 8, NW> st;
+  __amdgpu_buffer_rsrc_t rd = rb;
+  if constexpr (LD) {
+    const bf16_t* dp = args.D + (long long)lpart * LDR * args.ldd;
+    rd = __builtin_amdgcn_make_buffer_rsrc((void*)dp, (short)0, (int)(((long long)(LDR - 1) * args.ldd + args.K) * 2),
+                                           0x00020000);
+    st.prepare(args.gb, args.ldd, 0, LDR, wave, lane);
+  }
   // K tile at k0 (never straddles K1: K1 % 64 == 0) into the stage at img
   auto issue_tile = [&](char* img, int k0) {
     if (!SEG2 || k0 < args.K1) {
       sa.issue(ra, img, args.ga, args.lda, k0, SEG2 ? args.K1 : kend, wave);
       sb.issue(rb, img + ABYTES, args.gb, args.ldb, k0, SEG2 ? args.K1 : kend, wave);
+      if constexpr (LD) st.issue(rd, img + ABYTES + BBYTES, args.gb, args.ldd, k0, kend, wave);
     } else {
       sa2.issue(ra2, img, args.ga, args.lda2, k0 - args.K1, args.K2, wave);
       sb2.issue(rb2, img + ABYTES, args.gb, args.ldb2, k0 - args.K1, args.K2, wave);
@@ -308,7 +337,19 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
 #pragma unroll
     for (int j = 0; j < NJ; ++j) f[j] = BKm ? frag_k2(ib, wn * TN + j * 16, 32 * h) : frag_mn2<BN * 2>(ib, wn * TN + j * 16, 32 * h);
   };
-  auto mfma_block = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ]) {
+  // down-projection fusion: this wave's t blocks (rows i of its row range, its RCW column fragments of the part)
+  constexpr int NBT1 = NBT > 0 ? NBT : 1, RCW1 = RCW > 0 ? RCW : 1;
+  float4v acc_t[NBT1];
+#pragma unroll
+  for (int b = 0; b < NBT1; ++b) acc_t[b] = float4v{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ft0[RCW1], ft1[RCW1];
+  auto load_t = [&](bf16x8 (&f)[RCW1], const char* it, int h) {
+    if constexpr (LD) {
+#pragma unroll
+      for (int c = 0; c < RCW; ++c) f[c] = frag_k2(it, (wn * RCW + c) * 16, 32 * h);
+    }
+  };
+  auto mfma_block = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ], const bf16x8 (&ft)[RCW1]) {
     if constexpr (OTAMD_GEMM_ABL == 2) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[i]));
@@ -320,6 +361,13 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    if constexpr (LD) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int c = 0; c < RCW; ++c)
+          acc_t[i * RCW + c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft[c], fa[i], acc_t[i * RCW + c], 0, 0, 0);
+    }
   };
   // the next half's fragment reads (h = 0, load_b then load_a order) with this wave's refill DMA pieces of the slot
   // at dst placed one after each read: the inline-asm DMA keeps its place among the DS reads (both touch memory)
@@ -330,12 +378,17 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
   // colsum tiles (at their 128-VGPR cap) spilled 15 registers
   constexpr bool SPREAD = !SEG2 && NW == 8 && !(CS && BM == 128) && (AM == OPM_K || AM == OPM_MN) &&
                           (BMODE == OPM_K || BMODE == OPM_MN);
-  auto load_ab_refill = [&](bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ], const char* ia, const char* ib, char* dst, int k0) {
+  auto load_ab_refill = [&](bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ], bf16x8 (&ft)[RCW1], const char* ia, const char* ib,
+                            char* dst, int k0) {
     if constexpr (SPREAD) {
       auto piece = [&](int t) {   // offsets computed at the piece (no per-step offset arrays: the 256-wide tiles sit
                                   // at the 256-VGPR cap)
         if (t < NIA) sa.put(ra, dst, wave, t, sa.offset_g(args.ga, args.lda, k0, kend, t));
         else if (t < NIA + NIB) sb.put(rb, dst + ABYTES, wave, t - NIA, sb.offset_g(args.gb, args.ldb, k0, kend, t - NIA));
+        else if constexpr (LD) {
+          if (t < NIA + NIB + NIT)
+            st.put(rd, dst + ABYTES + BBYTES, wave, t - NIA - NIB, st.offset_g(args.gb, args.ldd, k0, kend, t - NIA - NIB));
+        }
       };
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -347,15 +400,23 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
         fa[i] = AK ? frag_k2(ia, wm * TM + i * 16, 0) : frag_mn2<BM * 2>(ia, wm * TM + i * 16, 0);
         piece(NJ + i);
       }
+      if constexpr (LD) {
 #pragma unroll
-      for (int t = MI + NJ; t < NIA + NIB; ++t) piece(t);
+        for (int c = 0; c < RCW; ++c) {
+          ft[c] = frag_k2(ib + BBYTES, (wn * RCW + c) * 16, 0);
+          piece(NJ + MI + c);
+        }
+      }
+#pragma unroll
+      for (int t = MI + NJ + RCW; t < NIA + NIB + NIT; ++t) piece(t);
     }
   };
   // interleave the next fragment reads into the current MFMA block: {2 MFMA, reads of 1 fragment} x (MI+NJ)
   // (128x128: 8 MFMAs per half for 6 fragment reads -> {1 MFMA, reads} x 6, then the rest)
-  constexpr int NR = MI + NJ;
-  constexpr int PER = (MI * NJ) / NR >= 2 ? 2 : 1;
-  constexpr int REST = MI * NJ - PER * NR;
+  constexpr int NR = MI + NJ + RCW;
+  constexpr int NMF = MI * NJ + NBT;
+  constexpr int PER = NMF / NR >= 2 ? 2 : 1;
+  constexpr int REST = NMF - PER * NR;
   auto interleave = [&]() {
 #pragma unroll
     for (int t = 0; t < NR; ++t) {
@@ -411,6 +472,7 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     BARRIER();
     load_b(fb0, smem + ABYTES, 0);
     load_a(fa0, smem, 0);
+    load_t(ft0, smem + ABYTES + BBYTES, 0);
     if constexpr (OTAMD_GEMM_ABL == 3) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) fa1[i] = fa0[i];
@@ -482,8 +544,9 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     if constexpr (OTAMD_GEMM_ABL != 3) {
       load_b(fb1, ib, 1);
       load_a(fa1, ia, 1);
+      load_t(ft1, ib + BBYTES, 1);
     }
-    mfma_block(fa0, fb0);
+    mfma_block(fa0, fb0, ft0);
     if constexpr (OTAMD_GEMM_ABL != 3) interleave();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -502,13 +565,14 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
     {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
       const char* na = smem + nstg * STAGE;
       if constexpr (OTAMD_GEMM_ABL != 3) {
-        if constexpr (REFILL && SPREAD) load_ab_refill(fa0, fb0, na, na + ABYTES, smem + stg * STAGE, kbeg + (kt + NS) * 64);
+        if constexpr (REFILL && SPREAD) load_ab_refill(fa0, fb0, ft0, na, na + ABYTES, smem + stg * STAGE, kbeg + (kt + NS) * 64);
         else {
           load_b(fb0, na + ABYTES, 0);
           load_a(fa0, na, 0);
+          load_t(ft0, na + ABYTES + BBYTES, 0);
         }
       }
-      mfma_block(fa1, fb1);
+      mfma_block(fa1, fb1, ft1);
       if constexpr (OTAMD_GEMM_ABL != 3) interleave();
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -521,6 +585,61 @@ __global__ void __launch_bounds__(NW * 64, (NS == 2 && BM == 128 && (BN == 128 |
   } else {   // conv gathers / the LoRA second segment: one body, the refill as a burst behind a uniform branch (a
              // peeled copy measured 4-8 % slower on the conv tiles)
     for (int kt = 0; kt < nk; ++kt) kstep(kt, std::true_type{});
+  }
+
+  if constexpr (LD) {   // the second K segment from the t accumulated above (no split-K: the launcher checks)
+    constexpr int KS2 = (LDR + 31) / 32;
+    const int g = lane >> 4;
+    // up-projection fragments of this wave's output columns (K-mode rows of U, 16 bytes per lane), loaded before the t
+    // hand-off so their latency hides behind it
+    bf16x8 fu[KS2][NJ];
+#pragma unroll
+    for (int s2 = 0; s2 < KS2; ++s2)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * TN + j * 16 + (lane & 15);
+        const int kk = 32 * s2 + 8 * g;
+        fu[s2][j] = bf16x8{};
+        if (n < args.N && kk < LDR)
+          fu[s2][j] = *reinterpret_cast<const bf16x8*>(args.B2 + (long long)n * args.ldb2 + lpart * LDR + kk);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    BARRIER();   // every wave is past its last stage read: stage 0 becomes the t image (BM rows x 64 k)
+    char* timg = smem;
+    const bool t_out = (n0 % args.lora_pw) == 0;   // the part's first tile column stores t for the backward
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int c = 0; c < RCW; ++c) {
+        const float4v v = acc_t[i * RCW + c];
+        const int row = wm * TM + i * 16 + (lane & 15);
+        const int col = (wn * RCW + c) * 16 + 4 * g;
+        uint2 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(timg + kimg_off(row, col >> 3) + (col & 7) * 2) = o;
+        const int m = m0 + row;
+        if (t_out && m < args.M) *reinterpret_cast<uint2*>(args.T + (long long)m * args.ldt + lpart * LDR + col) = o;
+      }
+    if constexpr (LDR % 32) {   // k in [LDR, 32 KS2): zeros (the up fragments there are zero; stale LDS bytes may be NaN)
+      constexpr int ZC = (32 - LDR % 32) / 8;   // 16-byte chunks per row
+      for (int e = threadIdx.x; e < BM * ZC; e += NW * 64) {
+        const int row = e / ZC, ch = LDR / 8 + e % ZC;
+        *reinterpret_cast<uint4*>(timg + kimg_off(row, ch)) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    BARRIER();
+#pragma unroll
+    for (int s2 = 0; s2 < KS2; ++s2) {
+      bf16x8 fa2[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa2[i] = frag_k2(timg, wm * TM + i * 16, 32 * s2);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[s2][j], fa2[i], acc[i][j], 0, 0, 0);
+    }
   }
 
   const bool use_slab = gridDim.z > 1;

@@ -13,6 +13,8 @@
 #include <torch/extension.h>
 
 #include <array>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <shared_mutex>
@@ -207,6 +209,75 @@ Tensor linear(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, co
   return o;
 }
 
+// ---- LoRA forward with the down-projection fused into the base GEMM (GemmArgs.D) ----
+// The plan is the measured one of the two-launch form's base GEMM (its second-segment signature); when that plan is a
+// one-split launch on a tile with a fused instance, one launch computes t (into t_out) and y.  Otherwise, or with
+// OTAMD_LORA_FUSE=0, the two launches: t = x down^T, then y with t as the second K segment.
+std::atomic<bool> g_lora_fuse{[] { const char* e = getenv("OTAMD_LORA_FUSE"); return !(e && e[0] == '0'); }()};
+bool lora_fuse_on() { return g_lora_fuse.load(std::memory_order_relaxed); }
+void set_lora_fuse(bool on) { g_lora_fuse.store(on); }
+std::atomic<long long> g_lora_fused{0}, g_lora_split{0};
+
+// Every tile column of a part recomputes the part's t (BM x r over all of K): r / BN more MFMA work in the base GEMM
+// (20-25 %), against the t GEMM's launch, its split-K reduce and two kernel boundaries.  In the C4 step the linear
+// forms gain from it and the 3x3 conv forms (K = 2880-11520, the t GEMM a small fraction of the base) lose, so convs
+// keep the two launches unless OTAMD_LORA_FUSE_CONV=1 (profiles/r6_lora_fused_ab.txt).
+bool lora_fuse_conv() {
+  static const bool v = [] { const char* e = getenv("OTAMD_LORA_FUSE_CONV"); return e && e[0] == '1'; }();
+  return v;
+}
+
+bool lora_down_fused(GemmArgs& a, const Tensor& down2d, const Tensor& up2, const Tensor& t2d, int64_t k1, int64_t r,
+                     int64_t pw, int64_t stream) {
+  if (!lora_fuse_on() || r != 32 || pw <= 0 || a.N % pw || k1 % 64) return false;
+  if (a.amode == OPM_CONV_FWD && !lora_fuse_conv()) return false;
+  GemmArgs k = a;   // the two-launch form's base GEMM signature (plan table key)
+  if (!seg2(k, t2d, up2, k1, false)) return false;
+  int tile = 0, splits = 0;
+  if (!lookup_plan(tune_key(k), tile, splits)) {
+    tile = otamd_gemm_plan_tile(&k, 0);
+    if (otamd_gemm_plan(&k, 0, &splits) < 0) return false;
+  }
+  if (splits != 1) return false;
+  if (tile == 0) tile = 4;   // no fused 256x256 instance (register cap): the 128x128 tile
+  req(is_bf16(down2d) && is_bf16(up2) && is_bf16(t2d) && aligned(down2d) && aligned(up2) && aligned(t2d),
+      "LoRA operands bf16, aligned");
+  a.D = down2d.data_ptr(); a.ldd = ld_rows(down2d);
+  a.B2 = up2.data_ptr(); a.ldb2 = ld_rows(up2);
+  a.T = t2d.data_ptr(); a.ldt = ld_rows(t2d);
+  a.lora_r = (int)r; a.lora_pw = (int)pw;
+  const int rc = otamd_gemm_explicit(&a, tile, 1, nullptr, 0, S(stream));
+  if (rc == OTAMD_EUNSUPPORTED) {
+    a.D = nullptr; a.B2 = nullptr; a.T = nullptr;
+    return false;
+  }
+  check(rc, "otamd_gemm_explicit (LoRA down fused)");
+  return true;
+}
+
+Tensor linear_lora(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, const optional<Tensor>& residual,
+                   const Tensor& down, const Tensor& up2, const Tensor& t_out, int64_t r, int64_t pw, int64_t stream) {
+  req(is_bf16(x) && is_bf16(w) && x.is_cuda() && x.dim() == 2 && w.dim() == 2, "linear_lora: bf16 2-D");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  req(K == w.size(1) && K % 8 == 0 && N % 4 == 0 && aligned(x) && aligned(w), "linear_lora shapes");
+  req(down.dim() == 2 && down.size(1) == K && up2.dim() == 2 && up2.size(0) == N && up2.size(1) == down.size(0) &&
+      t_out.dim() == 2 && t_out.size(0) == M && t_out.size(1) == down.size(0), "linear_lora: LoRA shapes");
+  Tensor o = out2d({}, M, N, at::kBFloat16, x);
+  GemmArgs a = new_args();
+  a.A = x.data_ptr(); a.lda = ld_rows(x); a.amode = OPM_K;
+  a.B = w.data_ptr(); a.ldb = ld_rows(w); a.bmode = OPM_K;
+  a.C = o.data_ptr(); a.ldc = M > 1 ? o.stride(0) : N;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  epilogue(a, bias, {}, 0, residual, M, N);
+  if (lora_down_fused(a, down, up2, t_out, K, r, pw, stream)) {
+    ++g_lora_fused;
+    return o;
+  }
+  ++g_lora_split;
+  linear(x, down, {}, {}, {}, 0, t_out, false, 1.0, false, {}, {}, stream);
+  return linear(x, w, bias, residual, {}, 0, o, false, 1.0, false, t_out, up2, stream);
+}
+
 Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const optional<Tensor>& out, const optional<Tensor>& residual,
                     bool accumulate, const optional<Tensor>& lora_u, const optional<Tensor>& lora_a2, int64_t stream) {
   req(is_bf16(dy) && is_bf16(w), "linear_dgrad: bf16");
@@ -312,6 +383,39 @@ Tensor conv2d(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, in
   gemm(a, 0, x.device(), stream);
   if (lora_t && !fused) linear(*t2, *lora_b2, {}, {}, {}, 0, o.view({M, Cout}), false, 1.0, true, {}, {}, stream);
   return o;
+}
+
+// conv forward + LoRA with the down-projection (the base 3x3 geometry, in -> r) fused; t_out [N, P, Q, r]
+Tensor conv2d_lora(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, int64_t stride, int64_t pad,
+                   bool upsample, const optional<Tensor>& residual, const optional<Tensor>& rowvec, const Tensor& down,
+                   const Tensor& up2, const Tensor& t_out, int64_t r, int64_t stream) {
+  const Nhwc s = nhwc(x);
+  req(w.dim() == 4 && down.dim() == 4, "conv weight [Cout,KH,KW,Cin]");
+  const int64_t Cout = w.size(0), KH = w.size(1), KW = w.size(2);
+  req(w.size(3) == s.C && is_bf16(w) && w.is_contiguous() && Cout % 8 == 0 && aligned(x) && aligned(w), "conv weight");
+  req(down.size(1) == KH && down.size(2) == KW && down.size(3) == s.C && down.is_contiguous() && up2.dim() == 2 &&
+      up2.size(0) == Cout && up2.size(1) == down.size(0), "conv2d_lora: LoRA shapes");
+  auto pq = conv_out_hw(s.H, s.W, KH, stride, pad, upsample);
+  const int64_t Pp = pq.first, Q = pq.second, M = s.N * Pp * Q, Kc = KH * KW * s.C;
+  req(t_out.is_contiguous() && t_out.numel() == M * down.size(0), "conv2d_lora: t_out [N, P, Q, r]");
+  Tensor o = at::empty({s.N, Pp, Q, Cout}, x.options());
+  GemmArgs a = new_args();
+  a.A = x.data_ptr(); a.lda = 8; a.amode = OPM_CONV_FWD;
+  a.ga = geom(s.N, s.H, s.W, s.C, Pp, Q, KH, KW, stride, pad, upsample, s.ld);
+  a.B = w.data_ptr(); a.ldb = Kc; a.bmode = OPM_K;
+  a.C = o.data_ptr(); a.ldc = Cout;
+  a.M = (int)M; a.N = (int)Cout; a.K = (int)Kc;
+  optional<Tensor> res2;
+  if (residual) res2 = residual->reshape({M, Cout});
+  epilogue(a, bias, rowvec, rowvec ? Pp * Q : 0, res2, M, Cout);
+  Tensor t2 = t_out.view({M, down.size(0)});
+  if (lora_down_fused(a, down.view({down.size(0), Kc}), up2, t2, Kc, r, Cout, stream)) {
+    ++g_lora_fused;
+    return o;
+  }
+  ++g_lora_split;
+  conv2d(x, down, {}, stride, pad, upsample, {}, {}, t_out, {}, {}, 0, 0, stream);
+  return conv2d(x, w, bias, stride, pad, upsample, residual, rowvec, o, t_out, up2, 0, 0, stream);
 }
 
 Tensor conv2d_dgrad(const Tensor& dy, const Tensor& w, int64_t H, int64_t W, int64_t stride, int64_t pad,
@@ -554,6 +658,10 @@ PYBIND11_MODULE(_otamd_host, m) {
   m.def("linear_dgrad", &linear_dgrad);
   m.def("linear_wgrad", &linear_wgrad);
   m.def("conv2d", &conv2d);
+  m.def("linear_lora", &linear_lora);
+  m.def("conv2d_lora", &conv2d_lora);
+  m.def("set_lora_fuse", &set_lora_fuse);
+  m.def("lora_fused_counts", []() { return std::make_pair((long long)g_lora_fused, (long long)g_lora_split); });
   m.def("conv2d_dgrad", &conv2d_dgrad);
   m.def("conv2d_wgrad", &conv2d_wgrad);
   m.def("layernorm_fwd", &layernorm_fwd);

@@ -461,6 +461,122 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, rowvec=No
     return out
 
 
+_LORA_FUSE = {"on": os.environ.get("OTAMD_LORA_FUSE", "1") != "0",
+              "conv": os.environ.get("OTAMD_LORA_FUSE_CONV", "0") == "1"}
+
+
+def set_lora_fuse(on: bool) -> None:
+    """LoRA forward with the down-projection fused into the base GEMM (on) or as two launches (A/B, tests)."""
+    _LORA_FUSE["on"] = bool(on)
+    h = _host()
+    if h is not None:
+        h.set_lora_fuse(bool(on))
+
+
+def _lora_down_fused(a: GemmArgs, down2d, up2, t2d, k1: int, r: int, pw: int, device, tile=None) -> bool:
+    """one launch computing t = A down^T (into t2d) and y = A B^T + t up2^T (GemmArgs.D); False when the plan of the
+    two-launch form's base GEMM is not a one-split launch on a tile with a fused instance (ops_host.cpp
+    lora_down_fused).  tile: force the tile (tests)."""
+    if not _LORA_FUSE["on"] or r != 32 or pw <= 0 or a.N % pw or k1 % 64:
+        return False
+    if tile is None and a.amode == OPM_CONV_FWD and not _LORA_FUSE["conv"]:   # ops_host.cpp lora_fuse_conv
+        return False
+    k = GemmArgs.from_buffer_copy(a)
+    if not _seg2(k, t2d, up2, k1, False):
+        return False
+    if tile is None:
+        plan = _plan_table().get(_tune_key(k))
+        if plan is None:
+            s_out = C.c_int(0)
+            if lib().otamd_gemm_plan(C.byref(k), 0, C.byref(s_out)) < 0:
+                return False
+            plan = (lib().otamd_gemm_plan_tile(C.byref(k), 0), s_out.value)
+        tile, splits = plan
+        if splits != 1:
+            return False
+        if tile == 0:   # no fused 256x256 instance (register cap): the 128x128 tile
+            tile = 4
+    _req(down2d.dtype == BF16 and up2.dtype == BF16 and t2d.dtype == BF16 and _aligned(down2d) and _aligned(up2)
+         and _aligned(t2d), "LoRA operands bf16, aligned")
+    a.D, a.ldd = _p(down2d), _ld_rows(down2d)
+    a.B2, a.ldb2 = _p(up2), _ld_rows(up2)
+    a.T, a.ldt = _p(t2d), _ld_rows(t2d)
+    a.lora_r, a.lora_pw = r, pw
+    rc = lib().otamd_gemm_explicit(C.byref(a), tile, 1, None, 0, stream_handle())
+    if rc == 3:   # OTAMD_EUNSUPPORTED: no fused instance for this tile / part width
+        a.D = a.B2 = a.T = None
+        return False
+    check(rc, "otamd_gemm_explicit (LoRA down fused)")
+    return True
+
+
+def linear_lora(x: torch.Tensor, w: torch.Tensor, bias, residual, down: torch.Tensor, up2: torch.Tensor,
+                t_out: torch.Tensor, rank: int, part_width: int, tile=None) -> torch.Tensor:
+    """LoRA forward of a frozen base Linear (LoRAModule.forward, modules/module/LoRAModule.py:318-322):
+    y = x w^T (+bias) (+residual) + t up2^T with t = x down^T, t written to t_out [M, P*r] for the backward.  One
+    launch with the down-projection inside the base GEMM's K loop when the plan allows (part_width = output columns
+    per adapter part, up2 block-diagonal over the parts), else t, then the base GEMM with t as its second K segment."""
+    h = _host()
+    if h is not None and tile is None:
+        return h.linear_lora(x, w, bias, residual, down, up2, t_out, rank, part_width, stream_handle())
+    _req(x.dtype == BF16 and w.dtype == BF16 and x.dim() == 2 and w.dim() == 2, "linear_lora: bf16 2-D")
+    M, Kd = x.shape
+    N = w.shape[0]
+    _req(w.shape[1] == Kd and Kd % 8 == 0 and N % 4 == 0 and _aligned(x) and _aligned(w), "linear_lora shapes")
+    _req(down.shape[1] == Kd and tuple(up2.shape) == (N, down.shape[0]) and tuple(t_out.shape) == (M, down.shape[0]),
+         "linear_lora: LoRA shapes")
+    out = torch.empty((M, N), dtype=BF16, device=x.device)
+    a = _new_args()
+    a.A, a.lda, a.amode = _p(x), _ld_rows(x), OPM_K
+    a.B, a.ldb, a.bmode = _p(w), _ld_rows(w), OPM_K
+    a.C, a.ldc = _p(out), out.stride(0) if M > 1 else N
+    a.M, a.N, a.K = M, N, Kd
+    _epilogue(a, bias, None, 0, residual, M, N)
+    if _lora_down_fused(a, down, up2, t_out, Kd, rank, part_width, x.device, tile=tile):
+        return out
+    linear(x, down, out=t_out)
+    return linear(x, w, bias=bias, residual=residual, out=out, lora=(t_out, up2))
+
+
+def conv2d_lora(x: torch.Tensor, w: torch.Tensor, bias, stride, pad, upsample, residual, rowvec, down: torch.Tensor,
+                up2: torch.Tensor, t_out: torch.Tensor, rank: int, tile=None) -> torch.Tensor:
+    """conv2d + LoRA (LoRAModule.py:142-155 conv branch: down = the base geometry in -> r, up = 1x1 r -> out) with the
+    down-projection fused into the base conv GEMM when the plan allows; t_out [N, P, Q, r]."""
+    h = _host()
+    if h is not None and tile is None:
+        return h.conv2d_lora(x, w, bias, stride, pad, upsample, residual, rowvec, down, up2, t_out, rank,
+                             stream_handle())
+    N, H, W, Cin, ldx = _nhwc(x)
+    Cout, KH, KW, Cin2 = w.shape
+    _req(Cin2 == Cin and w.dtype == BF16 and w.is_contiguous() and Cout % 8 == 0 and _aligned(x) and _aligned(w),
+         "conv weight [Cout,KH,KW,Cin]")
+    P, Q = conv_out_hw(H, W, KH, stride, pad, upsample)
+    M, Kc = N * P * Q, KH * KW * Cin
+    _req(tuple(down.shape[1:]) == (KH, KW, Cin) and tuple(up2.shape) == (Cout, down.shape[0]) and t_out.is_contiguous()
+         and t_out.numel() == M * down.shape[0], "conv2d_lora: LoRA shapes")
+    out = torch.empty((N, P, Q, Cout), dtype=BF16, device=x.device)
+    a = _new_args()
+    a.A, a.lda, a.amode = _p(x), 8, OPM_CONV_FWD
+    a.ga = _geom(N, H, W, Cin, P, Q, KH, KW, stride, pad, upsample, ldx)
+    a.B, a.ldb, a.bmode = _p(w), Kc, OPM_K
+    a.C, a.ldc = _p(out), Cout
+    a.M, a.N, a.K = M, Cout, Kc
+    res2 = residual.reshape(M, Cout) if residual is not None else None
+    _epilogue(a, bias, rowvec, P * Q if rowvec is not None else 0, res2, M, Cout)
+    if _lora_down_fused(a, down.view(down.shape[0], Kc), up2, t_out.view(M, down.shape[0]), Kc, rank, Cout, x.device,
+                        tile=tile):
+        return out
+    conv2d(x, down, stride=stride, pad=pad, upsample=upsample, out=t_out)
+    return conv2d(x, w, bias=bias, stride=stride, pad=pad, upsample=upsample, residual=residual, rowvec=rowvec, out=out,
+                  lora=(t_out, up2))
+
+
+def lora_fused_counts() -> tuple:
+    """(fused, two-launch) LoRA forwards issued by the native host layer since load."""
+    h = _host()
+    return tuple(h.lora_fused_counts()) if h is not None else (0, 0)
+
+
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, accumulate=False,
                  lora=None) -> torch.Tensor:
     """dx[M,K] = dy[M,N] @ w[N,K].  lora = (u [M,r], a2 [r,K]): dx += u @ a2 (second K segment)."""

@@ -170,8 +170,8 @@ def _trainable_params(*refs):
 
 class LoraLinearFn(torch.autograd.Function):
     """y = x W^T (+b) (+residual) + s * (x A^T) B^T with a frozen base (LoRAModule.forward,
-    modules/module/LoRAModule.py:318-322).  Forward: t = x A^T (skinny GEMM), then the base GEMM
-    with [t | s B] as its second K segment.  Backward: u = dy (sB); dx = [dy | u] [W ; A] (one
+    modules/module/LoRAModule.py:318-322).  Forward: one launch with t = x A^T accumulated in the base GEMM's K loop
+    and [t | s B] as its second K segment (kernels.linear_lora; two launches where the plan does not allow it).  Backward: u = dy (sB); dx = [dy | u] [W ; A] (one
     GEMM); dA = u^T x; dB_p = s dy_p^T t_p per fused part; all adapter grads fp32."""
 
     @staticmethod
@@ -179,8 +179,9 @@ class LoraLinearFn(torch.autograd.Function):
         shp = x.shape
         x2 = _rows(x)
         r2 = _rows(residual) if residual is not None else None
-        t = K.linear(x2, site.down)
-        y = K.linear(x2, wref.w, bias=bref.w if bref is not None else None, residual=r2, lora=(t, site.up2))
+        t = torch.empty((x2.shape[0], site.down.shape[0]), dtype=x2.dtype, device=x2.device)
+        y = K.linear_lora(x2, wref.w, bref.w if bref is not None else None, r2, site.down, site.up2, t, site.rank,
+                          site.part_width)
         ctx.save_for_backward(x2, t)
         ctx.wref, ctx.bref, ctx.site, ctx.has_res, ctx.xshape = wref, bref, site, residual is not None, shp
         return y.view(*shp[:-1], wref.w.shape[0])
@@ -271,9 +272,10 @@ class LoraConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wref, bref, rowvec, residual, stride, upsample, site, *params):
-        t = K.conv2d(x, site.down, stride=stride, pad=1, upsample=upsample)
-        y = K.conv2d(x, wref.w, bias=bref.w if bref is not None else None, stride=stride, pad=1, upsample=upsample,
-                     residual=residual, rowvec=rowvec, lora=(t, site.up2))
+        Ho, Wo = K.conv_out_hw(x.shape[1], x.shape[2], site.k, stride, 1, upsample)
+        t = torch.empty((x.shape[0], Ho, Wo, site.down.shape[0]), dtype=x.dtype, device=x.device)
+        y = K.conv2d_lora(x, wref.w, bref.w if bref is not None else None, stride, 1, upsample, residual, rowvec,
+                          site.down, site.up2, t, site.rank)
         ctx.save_for_backward(x, t)
         ctx.wref, ctx.bref, ctx.stride, ctx.upsample, ctx.site = wref, bref, stride, upsample, site
         ctx.has_rowvec, ctx.has_res = rowvec is not None, residual is not None

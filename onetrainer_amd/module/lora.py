@@ -60,6 +60,17 @@ class LoraSite:
     params: tuple = ()
     group: tuple = ()        # all modules of the base GEMM (adapted or not)
 
+    @property
+    def part_width(self) -> int:
+        """output columns per adapted part when the parts tile the fused GEMM's columns evenly (every module of the
+        group adapted, equal widths): the down-projection can then run inside the base GEMM (kernels.linear_lora);
+        0 otherwise."""
+        P = len(self.modules)
+        if P == 0 or self.n_total % P:
+            return 0
+        pw = self.n_total // P
+        return pw if list(self.ranges) == [(p * pw, (p + 1) * pw) for p in range(P)] else 0
+
     def acc(self) -> bool:
         return self.store.accumulate_into(self.names)
 
