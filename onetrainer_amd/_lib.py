@@ -192,6 +192,10 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = C.c_longlong if name.endswith(("_ws_floats", "_ws_bytes", "_slab_bytes", "_plan", "_part_floats")) else C.c_int
+        if L.otamd_gemm_args_size() != C.sizeof(GemmArgs):   # an older build (or OTAMD_LIB_ALT revision) with another
+            # GemmArgs layout would read the struct short and silently drop fields (e.g. the fused LoRA operands)
+            raise RuntimeError(f"{path.name}: GemmArgs is {L.otamd_gemm_args_size()} bytes, this package's is "
+                               f"{C.sizeof(GemmArgs)}: rebuild it (python -m onetrainer_amd.build)")
         _lib = L
     return _lib
 

@@ -376,15 +376,20 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
   // plain K / MN operands only: with a conv gather the per-piece offset arithmetic (integer divisions) inside phase B
   // cost more than the burst (conv fwd / dgrad 10-15 % slower, profiles/r4_gemm_spread_conv_*), and the 128-row
   // colsum tiles (at their 128-VGPR cap) spilled 15 registers
-  constexpr bool SPREAD = !SEG2 && NW == 8 && !(CS && BM == 128) && (AM == OPM_K || AM == OPM_MN) &&
+  // The LoRA second segment (SEG2) spreads the refills of its first segment too; the few refills that land in the
+  // second segment (K2 <= 64 rows: one K-step) go out as a burst through issue_tile.  Not the 128x160 dgrad form with
+  // a second segment: at its 128-VGPR cap the spread pushed it to 20 bytes of scratch per lane.
+  constexpr bool SPREAD = NW == 8 && !(CS && BM == 128) && !(SEG2 && BM == 128 && BN == 160 && BMODE == OPM_MN) &&
+                          (AM == OPM_K || AM == OPM_MN) &&
                           (BMODE == OPM_K || BMODE == OPM_MN);
   auto load_ab_refill = [&](bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ], bf16x8 (&ft)[RCW1], const char* ia, const char* ib,
                             char* dst, int k0) {
     if constexpr (SPREAD) {
       auto piece = [&](int t) {   // offsets computed at the piece (no per-step offset arrays: the 256-wide tiles sit
                                   // at the 256-VGPR cap)
-        if (t < NIA) sa.put(ra, dst, wave, t, sa.offset_g(args.ga, args.lda, k0, kend, t));
-        else if (t < NIA + NIB) sb.put(rb, dst + ABYTES, wave, t - NIA, sb.offset_g(args.gb, args.ldb, k0, kend, t - NIA));
+        const int k1end = SEG2 ? args.K1 : kend;
+        if (t < NIA) sa.put(ra, dst, wave, t, sa.offset_g(args.ga, args.lda, k0, k1end, t));
+        else if (t < NIA + NIB) sb.put(rb, dst + ABYTES, wave, t - NIA, sb.offset_g(args.gb, args.ldb, k0, k1end, t - NIA));
         else if constexpr (LD) {
           if (t < NIA + NIB + NIT)
             st.put(rd, dst + ABYTES + BBYTES, wave, t - NIA - NIB, st.offset_g(args.gb, args.ldd, k0, kend, t - NIA - NIB));
@@ -534,8 +539,12 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
   // after the barrier they held the issuing wave for the whole burst (~60-185 cycles per 1-KiB piece,
   // MI355X_MICROARCH.md) with its MFMAs waiting behind it.  The K steps without a refill (the last NS) run a copy
   // of the body with no DMA at all, so no branch splits phase B's scheduling region.
+  // refill_tag: 0 = no refill, 1 = refill (spread through phase B where SPREAD, else a burst), 2 = refill as a burst
   auto kstep = [&](int kt, auto refill_tag) {
-    constexpr bool REFILL = decltype(refill_tag)::value && OTAMD_GEMM_ABL != 1;
+    constexpr int RM = decltype(refill_tag)::value;
+    constexpr bool REFILL = RM != 0 && OTAMD_GEMM_ABL != 1;
+    constexpr bool BURST = REFILL && (RM == 2 || !SPREAD);
+    constexpr bool SPREAD_NOW = REFILL && RM == 1 && SPREAD;
     const char* ia = smem + stg * STAGE;
     const char* ib = ia + ABYTES;
     const int nstg = stg + 1 == NS ? 0 : stg + 1;
@@ -553,7 +562,7 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
     // tile kt+1 has landed: the tiles after it that may still be in flight are kt+2 .. min(kt+NS-1, nk-1)
     wait_tiles(min(NS - 2, nk - kt - 2));
     if constexpr (OTAMD_GEMM_ABL != 4) BARRIER();
-    if constexpr (REFILL && !SPREAD) {   // refill tile kt's slot
+    if constexpr (BURST) {   // refill tile kt's slot
       if (kt + NS < nk) issue_tile(smem + stg * STAGE, kbeg + (kt + NS) * 64);
     }
     if constexpr (CS) {   // tile kt+1: published by this barrier, refilled only after the next one
@@ -565,7 +574,7 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
     {   // on the last step this reads a stale stage; harmless and keeps the loop branch-free
       const char* na = smem + nstg * STAGE;
       if constexpr (OTAMD_GEMM_ABL != 3) {
-        if constexpr (REFILL && SPREAD) load_ab_refill(fa0, fb0, ft0, na, na + ABYTES, smem + stg * STAGE, kbeg + (kt + NS) * 64);
+        if constexpr (SPREAD_NOW) load_ab_refill(fa0, fb0, ft0, na, na + ABYTES, smem + stg * STAGE, kbeg + (kt + NS) * 64);
         else {
           load_b(fb0, na + ABYTES, 0);
           load_a(fa0, na, 0);
@@ -580,11 +589,15 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
   };
   if constexpr (SPREAD) {
     int kt = 0;
-    for (; kt < nk - NS; ++kt) kstep(kt, std::true_type{});
-    for (; kt < nk; ++kt) kstep(kt, std::false_type{});
+    // SEG2: refills whose K-step lies in the second segment (k0 >= K1; K1 and kbeg are multiples of 64) burst
+    const int n_spread = SEG2 ? max(0, min(nk - NS, (args.K1 - kbeg) / 64 - NS)) : nk - NS;
+    for (; kt < n_spread; ++kt) kstep(kt, std::integral_constant<int, 1>{});
+    if constexpr (SEG2)
+      for (; kt < nk - NS; ++kt) kstep(kt, std::integral_constant<int, 2>{});
+    for (; kt < nk; ++kt) kstep(kt, std::integral_constant<int, 0>{});
   } else {   // conv gathers / the LoRA second segment: one body, the refill as a burst behind a uniform branch (a
              // peeled copy measured 4-8 % slower on the conv tiles)
-    for (int kt = 0; kt < nk; ++kt) kstep(kt, std::true_type{});
+    for (int kt = 0; kt < nk; ++kt) kstep(kt, std::integral_constant<int, 1>{});
   }
 
   if constexpr (LD) {   // the second K segment from the t accumulated above (no split-K: the launcher checks)
