@@ -417,6 +417,8 @@ def main():
                    "model": mname, "global_batch": args.batch * world,
                    "seq_len": (args.res // 8) ** 2, "parallelism": f"dp{world}"},
         "loss": round(loss_val, 5),
+        "loss_exact": loss_val,
+        "losses_exact": [float(v) for v in torch.stack(losses).float().cpu()],
         "lora_forwards_fused_vs_two_launch": list(K.lora_fused_counts()),
         "roofline": {"bound": "mfma", "achieved": round(g_achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(g_achieved / PEAK_BF16_TFLOPS, 4),

@@ -665,6 +665,9 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
         float4* q = reinterpret_cast<float4*>(red + cs_rg * BM + cs_c * 8);
         q[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
         q[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+        // the row-group partials are read by other waves: their ds_writes must retire before the barrier (gfx950's
+        // back-off barrier does not wait for LDS stores, and the compiler adds no waitcnt in front of a raw s_barrier)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         BARRIER();
       }
       for (int c = threadIdx.x; c < BM; c += NW * 64) {

@@ -105,6 +105,16 @@ class FusedAdamW(torch.optim.Optimizer):
         self.store.wait_params()   # the previous (overlapped) update still reads grads / clip_out
         nt = len(self.store.order)
         if self.norm_overlap is not None and self.norm_overlap.take():   # sums accumulated during backward
+            if _NORM_CHECK:   # debug: every overlapped chunk sum against the same pass over the final gradients
+                ref = torch.empty_like(self._chunk_sq)
+                _lib.check(_lib.lib().otamd_grad_sqnorm_chunks(self.store.grad.data_ptr(), self._norm_dtype,
+                                                               self._chunks.data_ptr(), 0, self._n_chunks,
+                                                               ref.data_ptr(), K.stream_handle()), "norm check")
+                bad = (ref != self._chunk_sq[:self._n_chunks]).nonzero().flatten().tolist()
+                if bad:
+                    names = sorted({self.store.order[self._chunk_tensor[c]] for c in bad})
+                    print(f"[norm check] {len(bad)} of {self._n_chunks} overlapped chunk sums differ from the final "
+                          f"gradients': {names[:12]}", flush=True)
             _lib.check(_lib.lib().otamd_grad_clip_finalize(self._chunks.data_ptr(), self._n_chunks,
                                                            self._chunk_sq.data_ptr(), self._tensor_sq.data_ptr(), nt,
                                                            float(max_norm), self._norm_dtype,
@@ -242,6 +252,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 idx += 1
 
 
+_NORM_CHECK = os.environ.get("OTAMD_NORM_CHECK") == "1"
+
+
 class OverlappedGradNorm:
     """clip_grad_norm_'s squared-norm pass spread over the backward.  Single process: gradient ranges of about
     `bucket_bytes` (whole tensors, reverse layout order = the order backward finishes them) are summed on the
@@ -304,6 +317,7 @@ class OverlappedGradNorm:
         self.armed = update_step
         self.ready = False
         self.pending = [len(b[2]) for b in self.buckets]
+        self._seen = set()
         self.launched = [False] * len(self.buckets)   # every bucket's chunk slots are rewritten each armed step
 
     def _launch(self, bi, side):
@@ -337,6 +351,13 @@ class OverlappedGradNorm:
         if not self.armed:
             return
         pending, bucket_of = self.pending, self.bucket_of
+        if _NORM_CHECK:   # debug: a gradient marked twice, or after its range was summed, would race the norm pass
+            for n in names:
+                if n in self._seen:
+                    raise RuntimeError(f"overlapped grad norm: {n} marked ready twice in one step")
+                if self.launched[bucket_of[n]]:
+                    raise RuntimeError(f"overlapped grad norm: {n} marked ready after its range was summed")
+                self._seen.add(n)
         for n in names:
             bi = bucket_of[n]
             pending[bi] -= 1
