@@ -16,8 +16,12 @@
 // Staging: every streamed tile (K/V for fwd and dQ, Q/dO and the {lse, delta} pairs for dK/dV)
 // goes HBM/L2 -> LDS by LDS-DMA (buffer_load ... lds) into an NS-deep ring, the swizzles applied
 // on the source address; one s_barrier per tile (RAW for tile t, WAR for the stage refilled
-// with tile t+NS-1).  Out-of-range rows / padded head columns are zero-filled by the
-// descriptor range check or an invalid offset.
+// with tile t+NS-1).  That barrier is BARRIER_LDS: gfx950's s_barrier does not wait for a wave's
+// outstanding ds_reads, and the compiler sinks the last MFMA of a tile (with the lgkmcnt wait for
+// its operand reads) below a raw s_barrier -- another wave's refill DMA then raced the reads it
+// had issued (dQ run-to-run differences under LDS contention from co-resident kernels, round 6).
+// Out-of-range rows / padded head columns are zero-filled by the descriptor range check or an
+// invalid offset.
 // Softmax VALU is kept under the MFMA time: single-issue fp32 math (no v_pk_*: they cost more than two
 // single ops beside MFMAs), key masking only on the partial last tile, and the forward's O rescale skipped
 // when no lane's max grew.
@@ -398,7 +402,7 @@ __global__ void __launch_bounds__(256, (D == 64 && NS == 2) ? 4 : 2) attn_fwd_ke
 
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
-    BARRIER();
+    BARRIER_LDS();   // WAR: this wave's reads of the slot refilled next have retired
     if (t + NS - 1 < ntiles) {
       char* st = smem + ((SI + NS - 1) % NS) * STG;
       ki.issue(rk, st, a.ldk, (t + NS - 1) * KT, a.Nk, a.Dv, wave);
@@ -567,7 +571,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 3 : 2) attn_bwd_dq_kernel(AttnA
 
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
-    BARRIER();
+    BARRIER_LDS();   // WAR: this wave's reads of the slot refilled next have retired
     if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
     const char* kimg = smem + SI * STG;
     const char* vimg = kimg + TB;
@@ -735,7 +739,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkv_kernel(AttnArgs a) {
     const int SI = si_tag;   // t % NS (a compile-time constant when unrolled)
     if (t + NS - 2 < ntiles) wait_vmcnt<(NS - 2) * LOADS>();
     else wait_vmcnt<0>();
-    BARRIER();
+    BARRIER_LDS();   // WAR: this wave's reads of the slot refilled next have retired
     if (t + NS - 1 < ntiles) issue(t + NS - 1, smem + ((SI + NS - 1) % NS) * STG);
     const char* st = smem + SI * STG;
 #pragma unroll 1

@@ -114,7 +114,8 @@ class GenericTrainer(TimedActionMixin):
         if (isinstance(opt, FusedAdamW) and self.graphs is None and self.config.clip_grad_norm
                 and opt.store.grad.is_cuda and S.enabled() and os.environ.get("OTAMD_NORM_OVERLAP", "1") != "0"
                 and opt.norm_overlap is None):
-            opt.norm_overlap = OverlappedGradNorm(opt, reducer=self.reducer)
+            opt.norm_overlap = OverlappedGradNorm(opt, reducer=self.reducer,
+                                                  bucket_bytes=int(os.environ.get("OTAMD_NORM_BUCKET_MB", "64")) << 20)
 
     def _load_weights(self):
         """base / VAE / LoRA weights and a backup to continue from (GenericTrainer.py:92-108 +
