@@ -1,14 +1,14 @@
 """Static check of gfx950 device assembly (not a test by itself; tests/test_lds_barriers.py runs it on attention.hip):
-every s_barrier must be reached with no LDS read of this wave outstanding.
+every s_barrier must be reached with no LDS access of this wave outstanding.
 
-Why: gfx950's s_barrier does not wait for a wave's outstanding ds_reads (nor ds_writes).  The ring kernels refill the
+Why: gfx950's s_barrier does not wait for a wave's outstanding ds_reads or ds_writes.  The ring kernels refill the
 slot read in the previous tile with LDS-DMA right after the barrier, so a wave that arrives with ds_reads still in
 flight lets another wave's DMA overwrite the data under them.  The compiler creates exactly that when it sinks the
 last MFMA of a tile -- and the lgkmcnt wait for its operands -- below a raw s_barrier (attn_bwd_dq_kernel<64, 3>
 before round 6: dQ differed run to run when co-resident kernels slowed its LDS reads).
 
-A forward data flow over each kernel's basic blocks: a ds_read counts as outstanding until an lgkmcnt wait that
-covers it, and a block starts with the most reads outstanding over its predecessors.
+A forward data flow over each kernel's basic blocks: an LDS access counts as outstanding until an lgkmcnt wait that
+covers it (a write published to other waves by the barrier is a RAW hazard just as a read is a WAR one), and a block starts with the most reads outstanding over its predecessors.
 
 usage: python tools/lds_barrier_check.py FILE.hip|FILE.s ...   (exit 1 on a hit)
 """
@@ -65,8 +65,9 @@ def _transfer(ins, pending):
     """-> (pending after the block, barriers, barriers reached with reads outstanding)"""
     nb = bad = 0
     for t in ins:
-        if t.startswith("ds_read") or t.startswith("ds_load"):
-            pending = min(pending + 1, 64)
+        if t.startswith("ds_") and not t.startswith("ds_nop") and not t.startswith("ds_swizzle") \
+                and not t.startswith("ds_bpermute") and not t.startswith("ds_permute"):
+            pending = min(pending + 1, 64)   # LDS reads, writes and atomics (lane permutes touch no LDS)
         w = re.search(r"s_waitcnt.*lgkmcnt\((\d+)\)", t)
         if w:
             n = int(w.group(1))
