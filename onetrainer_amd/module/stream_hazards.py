@@ -138,6 +138,8 @@ class StreamHazardCheck(TorchDispatchMode):
         sp = _span(t)
         if sp is None:
             return
+        if self._on_side():   # allocated on the side stream: its reuse is ordered by that stream, nothing to record
+            self.covered.add(t.untyped_storage().data_ptr())
         self.allocated.add(t.untyped_storage().data_ptr())
         lo, hi = sp
         self.pending = [p for p in self.pending if not (lo < p[1] and p[0] < hi)]
