@@ -158,6 +158,11 @@ def precomputed_linear(x, wref, y):
     return PrecomputedLinearFn.apply(x, wref, [y], *_params(wref))
 
 
+# a LoRA linear whose input needs no gradient runs its whole backward on the weight-gradient stream
+# (OTAMD_WGRAD_ONLY_SIDE=0: u = dy (sB) on the current stream, the A/B reference)
+_WONLY_SIDE = os.environ.get("OTAMD_WGRAD_ONLY_SIDE", "1") != "0"
+
+
 def linear(x, wref, bref=None, residual=None, lora=None):
     if lora is not None:
         return LoraLinearFn.apply(x, wref, bref, residual, lora, *lora.params, *_trainable_params(wref, bref))
@@ -190,12 +195,10 @@ class LoraLinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, t = ctx.saved_tensors
         wref, bref, site = ctx.wref, ctx.bref, ctx.site
-        dy2 = _rows(dy)
-        if dy2.stride(1) != 1 or dy2.stride(0) % 8:
-            dy2 = dy2.contiguous()
-        u = K.linear_dgrad(dy2, site.up2)
         btr = bref is not None and bref.trainable
-        with S.wgrad_region((dy2, x2, t, u)):
+        need_dx = ctx.needs_input_grad[0]
+
+        def wgrads(dy2, u):
             acc = site.acc()
             K.linear_wgrad(u, x2, out=site.g_down, accumulate=acc)
             r = site.rank
@@ -205,9 +208,25 @@ class LoraLinearFn(torch.autograd.Function):
                 K.linear_wgrad(dy2, x2, out=wref.g, accumulate=wref.acc())
             if btr:
                 K.colsum(dy2, out=bref.g.view(1, -1), accumulate=bref.acc())
+
         dx = None
-        if ctx.needs_input_grad[0]:
-            dx = K.linear_dgrad(dy2, wref.w, lora=(u, site.down)).view(ctx.xshape)
+        if not need_dx and _WONLY_SIDE and S.side_stream() is not None:
+            # no input gradient (the cross-attention K / V projection of text states that need none): u = dy (sB) is
+            # only a weight-gradient operand, so the whole backward goes to the weight-gradient stream
+            with S.wgrad_region((dy, x2, t)):
+                dy2 = _rows(dy)
+                if dy2.stride(1) != 1 or dy2.stride(0) % 8:
+                    dy2 = dy2.contiguous()
+                wgrads(dy2, K.linear_dgrad(dy2, site.up2))
+        else:
+            dy2 = _rows(dy)
+            if dy2.stride(1) != 1 or dy2.stride(0) % 8:
+                dy2 = dy2.contiguous()
+            u = K.linear_dgrad(dy2, site.up2)
+            with S.wgrad_region((dy2, x2, t, u)):
+                wgrads(dy2, u)
+            if need_dx:
+                dx = K.linear_dgrad(dy2, wref.w, lora=(u, site.down)).view(ctx.xshape)
         site.done()
         if wref.trainable:
             wref.done()
@@ -489,8 +508,8 @@ _CROSS_CAST_SIDE = os.environ.get("OTAMD_CROSS_CAST_SIDE", "1") != "0"
 
 class CrossAttnFn(torch.autograd.Function):
     """q [B, N, C], kv [B, L, 2C] -> o [B, N, C].  kv_wgrad_only: every consumer of dkv runs on the weight-gradient
-    stream (kv from PrecomputedLinearFn over text states that need no gradient), so the one-pass backward's dK / dV
-    chunk sum (attn_dkv_cast) is queued there too, off the critical stream."""
+    stream (kv from PrecomputedLinearFn, or from a LoRA projection, over text states that need no gradient), so the
+    one-pass backward's dK / dV chunk sum (attn_dkv_cast) is queued there too, off the critical stream."""
 
     @staticmethod
     def forward(ctx, q, kv, heads, kv_wgrad_only=False):

@@ -390,8 +390,10 @@ class UNet2DConditionModel:
             kv = Fn.precomputed_linear(ehs, wkv, kv_pre)
         else:
             kv = Fn.linear(ehs, wkv, lora=self._lo_fused([p + ".attn2.to_k", p + ".attn2.to_v"]))
-        # dkv feeds only to_k|to_v's weight gradient (side stream) when the text states need no gradient
-        o = Fn.CrossAttnFn.apply(q, kv, heads, kv_pre is not None and not ehs.requires_grad)
+        # dkv feeds only to_k|to_v's weight gradient (side stream) when the text states need no gradient: the batched
+        # projection's (PrecomputedLinearFn) or the LoRA one's (LoraLinearFn runs its whole backward there then)
+        o = Fn.CrossAttnFn.apply(q, kv, heads, (kv_pre is not None or (self.lora is not None and Fn._WONLY_SIDE))
+                                 and not ehs.requires_grad)
         h = self._linear(o, p + ".attn2.to_out.0", residual=h)
         n3, h = Fn.layer_norm_res(h, self.R(p + ".norm3.weight"), self.R(p + ".norm3.bias"))
         g = self._linear(n3, p + ".ff.net.0.proj")
