@@ -65,7 +65,10 @@ typedef struct GemmArgs {
      rounded to bf16, stored to T [M][ldt] by the part's first tile column, and t (B2)^T added as the second K
      segment -- replaces the separate down GEMM x A^T + its split-K reduce before the fused up projection
      (LoRAModule.forward, modules/module/LoRAModule.py:318-322).  D = down [P*lora_r][K], B2 / ldb2 = up [N][P*lora_r],
-     lora_pw = output columns per part; K = the base K, A2 = NULL.  D == NULL: off. */
+     lora_pw = output columns per part; K = the base K, A2 = NULL.  D == NULL: off.
+     The same fields on a linear input-gradient GEMM (A = dY K-mode, B = W MN-mode): u = dY (sB) for one adapter part
+     spanning N (lora_pw = N), D = (sB)^T [lora_r][K], B2 / ldb2 = A^T [N][lora_r], T = u [M][ldt] -- the LoRA
+     backward's dX = dY W + u A (LoRAModule.py:318-322 differentiated) without the separate u GEMM and its reduce. */
   const void* D; long long ldd;
   void* T; long long ldt;
   int lora_r, lora_pw;
@@ -326,7 +329,8 @@ int otamd_cast_f32(const float* x, void* y, long long n, int dst_f32, int accumu
 
 /* replaces: the per-forward autocast casts of every LoRA down/up weight (LoRAModule.forward under
    autocast, modules/module/LoRAModule.py:318-322) -- one launch refreshes all bf16 shadows.
-   table: device array of {long long src, dst; int rows, cols, dst_ld; float scale} */
+   table: device array of {long long src, dst; int rows, cols, dst_ld; float scale; int transpose, pad}
+   (transpose = 1: the [rows][cols] source lands as [cols][rows] with row stride dst_ld) */
 int otamd_lora_shadow(const float* src, void* dst, const void* table, int n_entries, hipStream_t s);
 
 /* replaces: ABI check */

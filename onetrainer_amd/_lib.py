@@ -51,7 +51,7 @@ class NormChunk(C.Structure):
 
 class LoraShadowEntry(C.Structure):
     _fields_ = [("src", C.c_longlong), ("dst", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
-                ("dst_ld", C.c_int), ("scale", C.c_float)]
+                ("dst_ld", C.c_int), ("scale", C.c_float), ("transpose", C.c_int), ("pad", C.c_int)]
 
 
 class AttnArgs(C.Structure):

@@ -207,14 +207,16 @@ __global__ void conv_wt_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict_
 // LoRA bf16 shadow refresh (one launch per step for every adapter): entry e copies a [rows x cols]
 // fp32 block at src + e.src (contiguous) to bf16 at dst + e.dst with row stride e.dst_ld, times
 // e.scale (alpha / rank for up projections; fused q|k|v ups land on the diagonal of one [3C x 3r]).
-struct LoraShadowEntry { long long src, dst; int rows, cols, dst_ld; float scale; };
+// transpose = 1: the [rows][cols] source lands as [cols][rows] (row stride dst_ld): the transposed up / down copies
+// the fused LoRA input-gradient GEMM reads in K-mode (gemm2_kernel.h)
+struct LoraShadowEntry { long long src, dst; int rows, cols, dst_ld; float scale; int transpose, pad; };
 __global__ void __launch_bounds__(256) lora_shadow_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
                                                           const LoraShadowEntry* __restrict__ tab) {
   const LoraShadowEntry e = tab[blockIdx.y];
   const long long n = (long long)e.rows * e.cols;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const long long r = i / e.cols, c = i - r * e.cols;
-    dst[e.dst + r * e.dst_ld + c] = f2bf(src[e.src + i] * e.scale);
+    dst[e.dst + (e.transpose ? c * e.dst_ld + r : r * e.dst_ld + c)] = f2bf(src[e.src + i] * e.scale);
   }
 }
 

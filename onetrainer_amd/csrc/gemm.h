@@ -48,7 +48,8 @@ struct GemmArgs {
   // LoRA down-projection fused into the K loop of a forward base GEMM (v2 tiles, gemm2_tiles_e.hip): D = down
   // [P*lora_r][K] (K-mode, the K layout of B), B2 / ldb2 = up [N][P*lora_r] (alpha/rank folded in), T = t [M][ldt]
   // (bf16 out, for the backward), lora_pw = output columns per adapter part (tiles never straddle parts).  K is the
-  // base K (no second segment operand A2).  D == nullptr: off.
+  // base K (no second segment operand A2).  D == nullptr: off.  On a linear dgrad (B = W MN-mode): u = dY (sB) with
+  // D = (sB)^T [lora_r][K], B2 = A^T [N][lora_r], T = u, lora_pw = N (the LoRA backward's dX, include/otamd.h).
   const bf16_t* D; long long ldd;
   bf16_t* T; long long ldt;
   int lora_r, lora_pw;

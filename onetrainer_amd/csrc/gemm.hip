@@ -648,10 +648,11 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
   GemmArgs a = *in;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.N % 4) != 0 || splits < 0) return OTAMD_EINVAL;
   const bool v2_only = a.bmode == OPM_CONV_WT || a.A2 != nullptr || a.D != nullptr;
-  if (a.D) {   // LoRA down-projection fused into a forward base GEMM (gemm2_tiles_e.hip)
+  if (a.D) {   // LoRA projection fused into a base GEMM: forward t = x A^T, or the dgrad's u = dY (sB) (gemm2_tiles_e.hip)
     if (a.A2 || !a.B2 || !a.T || a.lora_r != 32 || a.lora_pw <= 0 || a.N % a.lora_pw || a.batch > 1 || a.colsum)
       return OTAMD_EINVAL;
-    if (!((a.amode == OPM_K || a.amode == OPM_CONV_FWD) && a.bmode == OPM_K)) return OTAMD_EUNSUPPORTED;
+    if (!((a.amode == OPM_K || a.amode == OPM_CONV_FWD) && a.bmode == OPM_K) && !(a.amode == OPM_K && a.bmode == OPM_MN))
+      return OTAMD_EUNSUPPORTED;
     if ((a.ldd % 8) || (a.ldb2 % 8) || (a.ldt % 8) || !aligned16(a.D) || !aligned16(a.B2) || !aligned16(a.T))
       return OTAMD_EINVAL;
   }

@@ -241,6 +241,10 @@ __device__ __forceinline__ int mn_chunk_off(int k, int c) {   // 16-byte chunk c
 // segment of the SEG2 form, without the t GEMM, its split-K reduce and their two launch boundaries.  The t sums run
 // over K in the same 64-deep steps and 16x16x32 MFMAs as a one-split t GEMM, so t, and y, are bit-identical to that
 // path.  LD tiles use 2 waves along N (wave tiles (BM / 4) x (BN / 2)), so each wave owns whole t column fragments.
+// The same instance with B = MN-mode weights is the LoRA backward's input gradient (one adapter part spanning N,
+// lora_pw = N): u = dY (sB) accumulated over the dgrad's K loop from D = (sB)^T [LDR][K], stored to T for the down
+// projection's weight gradient, and dX = dY W + u A with B2 = A^T [N][LDR] -- the u GEMM, its split-K reduce and the
+// second-segment DMA of the two-launch form (u GEMM + SEG2 dgrad) in one launch, bit-identical to it at one split.
 template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2, bool CS = false, int LDR = 0>
 __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && (BN == 128 || BN == 160)) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
                                                                  unsigned a2_bytes, unsigned b2_bytes) {
@@ -256,8 +260,9 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
   constexpr int RCW = LD ? RC / WN : 0;      // ... owned by one wave
   constexpr int NBT = MI * RCW;              // 16 x 16 t blocks per wave
   constexpr int TBYTES = LD ? LDR * 128 : 0;
-  static_assert(!LD || (!SEG2 && !CS && NS == 2 && NW == 8 && BMODE == OPM_K && RC % WN == 0 && RCW >= 1),
-                "down-projection fusion: forward forms, 8 waves, whole t fragments per wave");
+  static_assert(!LD || (!SEG2 && !CS && NS == 2 && NW == 8 && (BMODE == OPM_K || BMODE == OPM_MN) && RC % WN == 0 &&
+                        RCW >= 1),
+                "LoRA projection fusion: linear / conv forward or linear dgrad, 8 waves, whole t fragments per wave");
   constexpr int STAGE = ABYTES + BBYTES + TBYTES;
   constexpr int NIT = LD ? Stage<OPM_K, LD ? LDR : 8, NW>::NI : 0;
   constexpr int LOADS = Stage<AM, BM, NW>::NI + Stage<BMODE, BN, NW>::NI + NIT;

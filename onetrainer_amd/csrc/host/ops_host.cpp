@@ -297,6 +297,60 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const optional<Tensor>& o
   return o;
 }
 
+// ---- LoRA backward input gradient with u = dY (sB) fused into the dgrad GEMM (GemmArgs.D on a B = MN-mode GEMM) ----
+// One adapter (a single-module linear site): dX = dY W + u A and u (into u_out, for the down projection's weight
+// gradient) in one launch when the two-launch form's dgrad plan is a one-split launch on a tile with a fused instance
+// and N (= in features) is a multiple of its width; otherwise (or with OTAMD_LORA_FUSE=0 / OTAMD_LORA_FUSE_DGRAD=0) the
+// two launches: u = dY (sB), then dX with u as the second K segment.  Bit-identical either way at one split.
+bool lora_fuse_dgrad() {
+  static const bool v = [] { const char* e = getenv("OTAMD_LORA_FUSE_DGRAD"); return !(e && e[0] == '0'); }();
+  return v;
+}
+std::atomic<long long> g_lora_dgrad_fused{0}, g_lora_dgrad_split{0};
+
+Tensor linear_dgrad_lora(const Tensor& dy, const Tensor& w, const Tensor& up2, const Tensor& down, const Tensor& upT,
+                         const Tensor& downT, const Tensor& u_out, int64_t stream) {
+  req(is_bf16(dy) && is_bf16(w) && dy.dim() == 2 && w.dim() == 2, "linear_dgrad_lora: bf16 2-D");
+  const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1), r = up2.size(1);
+  req(N == w.size(0) && N % 8 == 0 && K % 8 == 0 && aligned(dy) && aligned(w), "linear_dgrad_lora shapes");
+  req(up2.dim() == 2 && up2.size(0) == N && down.dim() == 2 && down.size(0) == r && down.size(1) == K &&
+      upT.dim() == 2 && upT.size(0) == r && upT.size(1) == N && downT.dim() == 2 && downT.size(0) == K &&
+      downT.size(1) == r && u_out.dim() == 2 && u_out.size(0) == M && u_out.size(1) == r, "linear_dgrad_lora: LoRA shapes");
+  if (lora_fuse_on() && lora_fuse_dgrad() && r == 32 && N % 64 == 0) {
+    Tensor o = out2d({}, M, K, at::kBFloat16, dy);
+    GemmArgs a = new_args();
+    a.A = dy.data_ptr(); a.lda = ld_rows(dy); a.amode = OPM_K;
+    a.B = w.data_ptr(); a.ldb = ld_rows(w); a.bmode = OPM_MN;
+    a.C = o.data_ptr(); a.ldc = M > 1 ? o.stride(0) : K;
+    a.M = (int)M; a.N = (int)K; a.K = (int)N;
+    GemmArgs k = a;   // the two-launch form's dgrad signature (plan table key)
+    req(seg2(k, u_out, down, N, true), "linear_dgrad_lora: second segment");
+    int tile = 0, splits = 0;
+    if (!lookup_plan(tune_key(k), tile, splits)) {
+      tile = otamd_gemm_plan_tile(&k, 0);
+      if (otamd_gemm_plan(&k, 0, &splits) < 0) splits = 0;
+    }
+    if (splits == 1) {
+      if (tile == 0) tile = 4;   // no fused 256x256 instance (register cap): the 128x128 tile
+      req(aligned(upT) && aligned(downT) && aligned(u_out) && is_bf16(upT) && is_bf16(downT) && is_bf16(u_out),
+          "LoRA operands bf16, aligned");
+      a.D = upT.data_ptr(); a.ldd = ld_rows(upT);
+      a.B2 = downT.data_ptr(); a.ldb2 = ld_rows(downT);
+      a.T = u_out.data_ptr(); a.ldt = ld_rows(u_out);
+      a.lora_r = (int)r; a.lora_pw = (int)K;
+      const int rc = otamd_gemm_explicit(&a, tile, 1, nullptr, 0, S(stream));
+      if (rc != OTAMD_EUNSUPPORTED) {
+        check(rc, "otamd_gemm_explicit (LoRA dgrad fused)");
+        ++g_lora_dgrad_fused;
+        return o;
+      }
+    }
+  }
+  ++g_lora_dgrad_split;
+  linear_dgrad(dy, up2, u_out, {}, false, {}, {}, stream);
+  return linear_dgrad(dy, w, {}, {}, false, u_out, down, stream);
+}
+
 void bias_grad_args(GemmArgs& a, const optional<Tensor>& bg, bool bias_acc, int64_t n) {
   if (bg) {
     req(bg->numel() == n && bg->is_contiguous() && (is_bf16(*bg) || is_f32(*bg)), "bias grad [N]");
@@ -659,6 +713,9 @@ PYBIND11_MODULE(_otamd_host, m) {
   m.def("linear_wgrad", &linear_wgrad);
   m.def("conv2d", &conv2d);
   m.def("linear_lora", &linear_lora);
+  m.def("linear_dgrad_lora", &linear_dgrad_lora);
+  m.def("lora_dgrad_fused_counts",
+        []() { return std::make_pair((long long)g_lora_dgrad_fused, (long long)g_lora_dgrad_split); });
   m.def("conv2d_lora", &conv2d_lora);
   m.def("set_lora_fuse", &set_lora_fuse);
   m.def("lora_fused_counts", []() { return std::make_pair((long long)g_lora_fused, (long long)g_lora_split); });

@@ -577,6 +577,66 @@ def lora_fused_counts() -> tuple:
     return tuple(h.lora_fused_counts()) if h is not None else (0, 0)
 
 
+_LORA_FUSE_DGRAD = os.environ.get("OTAMD_LORA_FUSE_DGRAD", "1") != "0"
+
+
+def linear_dgrad_lora(dy: torch.Tensor, w: torch.Tensor, up2: torch.Tensor, down: torch.Tensor, upT: torch.Tensor,
+                      downT: torch.Tensor, u_out: torch.Tensor, tile=None) -> torch.Tensor:
+    """LoRA backward input gradient of a frozen single-module Linear (LoRAModule.forward differentiated,
+    modules/module/LoRAModule.py:318-322): dx = dy w + u down with u = dy up2 (alpha/rank folded into up2) written to
+    u_out [M, r] for the down projection's weight gradient.  One launch with u accumulated inside the dgrad GEMM's K
+    loop (GemmArgs.D = upT = up2^T, B2 = downT = down^T) when the two-launch form's plan allows, else u, then the
+    dgrad with u as its second K segment; bit-identical either way at one split (ops_host.cpp linear_dgrad_lora).
+    tile: force the tile (tests)."""
+    h = _host()
+    if h is not None and tile is None:
+        return h.linear_dgrad_lora(dy, w, up2, down, upT, downT, u_out, stream_handle())
+    _req(dy.dtype == BF16 and w.dtype == BF16 and dy.dim() == 2 and w.dim() == 2, "linear_dgrad_lora: bf16 2-D")
+    M, N = dy.shape
+    Kd = w.shape[1]
+    r = up2.shape[1]
+    _req(w.shape[0] == N and N % 8 == 0 and Kd % 8 == 0 and _aligned(dy) and _aligned(w), "linear_dgrad_lora shapes")
+    _req(tuple(up2.shape) == (N, r) and tuple(down.shape) == (r, Kd) and tuple(upT.shape) == (r, N)
+         and tuple(downT.shape) == (Kd, r) and tuple(u_out.shape) == (M, r), "linear_dgrad_lora: LoRA shapes")
+    if _LORA_FUSE["on"] and _LORA_FUSE_DGRAD and r == 32 and N % 64 == 0:
+        out = torch.empty((M, Kd), dtype=BF16, device=dy.device)
+        a = _new_args()
+        a.A, a.lda, a.amode = _p(dy), _ld_rows(dy), OPM_K
+        a.B, a.ldb, a.bmode = _p(w), _ld_rows(w), OPM_MN
+        a.C, a.ldc = _p(out), out.stride(0) if M > 1 else Kd
+        a.M, a.N, a.K = M, Kd, N
+        k = GemmArgs.from_buffer_copy(a)
+        _req(_seg2(k, u_out, down, N, True), "linear_dgrad_lora: second segment")
+        splits = 1
+        if tile is None:
+            plan = _plan_table().get(_tune_key(k))
+            if plan is None:
+                s_out = C.c_int(0)
+                plan = (lib().otamd_gemm_plan_tile(C.byref(k), 0),
+                        s_out.value if lib().otamd_gemm_plan(C.byref(k), 0, C.byref(s_out)) >= 0 else 0)
+            tile, splits = plan
+            if tile == 0:   # no fused 256x256 instance (register cap): the 128x128 tile
+                tile = 4
+        if splits == 1:
+            _req(all(t.dtype == BF16 and _aligned(t) for t in (upT, downT, u_out)), "LoRA operands bf16, aligned")
+            a.D, a.ldd = _p(upT), _ld_rows(upT)
+            a.B2, a.ldb2 = _p(downT), _ld_rows(downT)
+            a.T, a.ldt = _p(u_out), _ld_rows(u_out)
+            a.lora_r, a.lora_pw = r, Kd
+            rc = lib().otamd_gemm_explicit(C.byref(a), tile, 1, None, 0, stream_handle())
+            if rc != 3:   # OTAMD_EUNSUPPORTED: no fused instance for this tile / width
+                check(rc, "otamd_gemm_explicit (LoRA dgrad fused)")
+                return out
+    linear_dgrad(dy, up2, out=u_out)
+    return linear_dgrad(dy, w, lora=(u_out, down))
+
+
+def lora_dgrad_fused_counts() -> tuple:
+    """(fused, two-launch) LoRA input gradients issued by the native host layer since load."""
+    h = _host()
+    return tuple(h.lora_dgrad_fused_counts()) if h is not None else (0, 0)
+
+
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out=None, residual=None, accumulate=False,
                  lora=None) -> torch.Tensor:
     """dx[M,K] = dy[M,N] @ w[N,K].  lora = (u [M,r], a2 [r,K]): dx += u @ a2 (second K segment)."""

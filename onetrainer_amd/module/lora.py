@@ -51,6 +51,9 @@ class LoraSite:
     n_total: int = 0         # fused GEMM output width
     down: torch.Tensor | None = None     # bf16 shadow [P*r, cin] or [r, k, k, cin]
     up2: torch.Tensor | None = None      # bf16 shadow [n_total, P*r] (block-diagonal, zero rows elsewhere), x alpha/r
+    upT: torch.Tensor | None = None      # bf16 shadow [r, n_total] = up2^T, and downT [cin, r] = down^T: the operands of
+    downT: torch.Tensor | None = None    # the fused backward input gradient (kernels.linear_dgrad_lora); single-module
+    #                                      linear sites at r = 32 only (the instances), else None
     g_down: torch.Tensor | None = None   # fp32 grad view, shape of `down`
     g_up: list = field(default_factory=list)   # fp32 grad views [cout_p, r]
     store: FlatParamStore | None = None
@@ -158,7 +161,8 @@ class LoRAWrapper:
             for mname, co in zip(s.modules, s.couts):
                 specs.append((f"{prefix}.{mname}.lora_up.weight", (co, rank), prefix))
         self.store = FlatParamStore(specs, dtype, torch.device(model.device))
-        # bf16 shadow: per site the fused down then the block-diagonal up
+        # bf16 shadow: per site the fused down then the block-diagonal up (+ their transposes for the fused backward
+        # input gradient on single-module linear sites)
         total = 0
         layout = []
         for s in sites:
@@ -168,10 +172,14 @@ class LoRAWrapper:
             doff = (total + 7) // 8 * 8
             uoff = (doff + dn + 7) // 8 * 8
             total = uoff + un
-            layout.append((doff, uoff))
+            toff = None
+            if s.kind == "linear" and len(s.group) == 1 and P == 1 and rank == 32:
+                toff = (total + 7) // 8 * 8                  # upT [r, n_total], then downT [cin, r]
+                total = toff + rank * s.n_total + s.cin * rank
+            layout.append((doff, uoff, toff))
         self.shadow = torch.zeros(total + 8, dtype=torch.bfloat16, device=model.device)
         entries = []
-        for s, (doff, uoff) in zip(sites, layout):
+        for s, (doff, uoff, toff) in zip(sites, layout):
             P = len(s.modules)
             dshape = (P * rank, s.cin) if s.kind == "linear" else (rank, s.k, s.k, s.cin)
             s.down = self.shadow[doff:doff + math.prod(dshape)].view(dshape)
@@ -188,9 +196,16 @@ class LoRAWrapper:
                 us = self.store.slots[s.names[P + p]]
                 entries.append((us.offset, uoff + s.ranges[p][0] * P * rank + p * rank, s.couts[p], rank, P * rank,
                                 self.scale))
+            if toff is not None:
+                s.upT = self.shadow[toff:toff + rank * s.n_total].view(rank, s.n_total)
+                s.downT = self.shadow[toff + rank * s.n_total:toff + rank * s.n_total + s.cin * rank].view(s.cin, rank)
+                us = self.store.slots[s.names[1]]
+                entries.append((us.offset, toff, s.n_total, rank, s.n_total, self.scale, 1))   # (s up)^T
+                entries.append((dslot.offset, toff + rank * s.n_total, rank, s.cin, rank, 1.0, 1))   # down^T
         arr = (_lib.LoraShadowEntry * len(entries))()
-        for i, (src, dst, rows, cols, ld, sc) in enumerate(entries):
+        for i, (src, dst, rows, cols, ld, sc, *tr) in enumerate(entries):
             arr[i].src, arr[i].dst, arr[i].rows, arr[i].cols, arr[i].dst_ld, arr[i].scale = src, dst, rows, cols, ld, sc
+            arr[i].transpose = tr[0] if tr else 0
         self._table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(model.device)
         self._n_entries = len(entries)
         if seed is not None:

@@ -119,3 +119,75 @@ def test_linear_lora_dispatch(dev):
     assert err < 1e-2, err
     want = x.float() @ w.float().t() + b.float() + t.float() @ up2.float().t()
     assert (y.float() - want).abs().max().item() / want.abs().max().item() < 2e-2
+
+
+# ---- backward input gradient with u = dy (sB) inside the dgrad GEMM (kernels.linear_dgrad_lora) ----
+@pytest.mark.parametrize("tile", [1, 4, 7, 8])
+@pytest.mark.parametrize("M,Nout,Kin", [(1000, 1280, 1280), (4096, 10240, 1280), (4096, 1280, 5120), (300, 640, 640)])
+def test_linear_dgrad_lora_fused_bitwise(dev, monkeypatch, tile, M, Nout, Kin):
+    """dx = dy W + u A and u = dy (sB), one launch, against the two-launch form at one split: bit-identical (u sums
+    over the same 64-deep K steps and 16x16x32 MFMAs as the u GEMM; the second segment adds the same bf16 u)."""
+    if Kin % BN[tile]:
+        pytest.skip("input width not a tile multiple: the launcher refuses (two-launch form)")
+    torch.manual_seed(24)
+    r = 32
+    dy, w = rnd(M, Nout, dev=dev), rnd(Nout, Kin, dev=dev, scale=0.05)
+    up2, down = rnd(Nout, r, dev=dev, scale=0.05), rnd(r, Kin, dev=dev, scale=0.05)
+    upT, downT = up2.t().contiguous(), down.t().contiguous()
+    u = torch.full((M, r), float("nan"), device=dev, dtype=BF)
+    dx = K.linear_dgrad_lora(dy, w, up2, down, upT, downT, u, tile=tile)
+
+    def ref():
+        u_ref = K.linear_dgrad(dy, up2)
+        return u_ref, K.linear_dgrad(dy, w, lora=(u_ref, down))
+    u_ref, dx_ref = two_launch_split1(monkeypatch, ref)
+    assert torch.equal(u, u_ref), (u.float() - u_ref.float()).abs().max().item()
+    assert torch.equal(dx, dx_ref), (dx.float() - dx_ref.float()).abs().max().item()
+    want = dy.float() @ w.float() + u_ref.float() @ down.float()
+    err = (dx.float() - want).abs().max().item() / want.abs().max().item()
+    assert err < 2e-2, err
+
+
+def test_linear_dgrad_lora_dispatch(dev):
+    """the planned path (native host layer) at an SDXL level-2 shape runs fused when its plan is one split, and the
+    two-launch fallback (set_lora_fuse(False)) gives the same u and dx bits at one split / the same product."""
+    torch.manual_seed(25)
+    M, Nout, Kin, r = 4096, 1280, 1280, 32
+    dy, w = rnd(M, Nout, dev=dev), rnd(Nout, Kin, dev=dev, scale=0.05)
+    up2, down = rnd(Nout, r, dev=dev, scale=0.05), rnd(r, Kin, dev=dev, scale=0.05)
+    upT, downT = up2.t().contiguous(), down.t().contiguous()
+    u = torch.empty((M, r), device=dev, dtype=BF)
+    f0 = K.lora_dgrad_fused_counts()
+    dx = K.linear_dgrad_lora(dy, w, up2, down, upT, downT, u)
+    f1 = K.lora_dgrad_fused_counts()
+    if K.host_layer() == "native":
+        assert f1[0] + f1[1] == f0[0] + f0[1] + 1, (f0, f1)
+    u2 = torch.empty_like(u)
+    K.set_lora_fuse(False)
+    try:
+        dx2 = K.linear_dgrad_lora(dy, w, up2, down, upT, downT, u2)
+    finally:
+        K.set_lora_fuse(True)
+    assert (u.float() - u2.float()).abs().max().item() <= 2 ** -7 * u2.float().abs().max().item()
+    err = (dx.float() - dx2.float()).abs().max().item() / dx2.float().abs().max().item()
+    assert err < 1e-2, err
+
+
+def test_lora_shadow_transposes(dev):
+    """the transposed shadows of single-module linear sites (r = 32) hold exactly up2^T and down^T"""
+    from onetrainer_amd.module import unet as U
+    from onetrainer_amd.module.lora import LoRAUNetWrapper
+    m = U.UNet2DConditionModel(U.tiny_sdxl_config(), dev, seed=1, trainable=False)
+    lw = LoRAUNetWrapper(m, rank=32, alpha=8.0, seed=0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    lw.store.data.copy_(torch.randn(lw.store.data.shape, generator=g, device=dev) * 0.1)
+    lw.refresh()
+    n = 0
+    for s in lw.sites:
+        if s.upT is None:
+            assert s.kind != "linear" or len(s.group) > 1
+            continue
+        n += 1
+        assert torch.equal(s.upT, s.up2.t()), s.key
+        assert torch.equal(s.downT, s.down.t()), s.key
+    assert n > 0
