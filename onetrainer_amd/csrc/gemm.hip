@@ -655,6 +655,8 @@ static int gemm_impl(const GemmArgs* in, int splits, int force_tile, void* works
       return OTAMD_EUNSUPPORTED;
     if ((a.ldd % 8) || (a.ldb2 % 8) || (a.ldt % 8) || !aligned16(a.D) || !aligned16(a.B2) || !aligned16(a.T))
       return OTAMD_EINVAL;
+    // dgrad form with K1 = rows per adapter part (u over several parts along K): whole 64-row K steps per part
+    if (a.K1 && (a.bmode != OPM_MN || a.K1 < 0 || a.K1 % 64 || a.K % a.K1)) return OTAMD_EINVAL;
   }
   if (a.A2) {   // second K segment (LoRA fusion): forms and alignment the v2 kernels support
     if (!a.B2 || a.K1 <= 0 || a.K2 <= 0 || a.K1 % 64 || a.K != a.K1 + a.K2) return OTAMD_EINVAL;

@@ -10,7 +10,7 @@ gemm2_fn gemm2_pick_a(int tile, int am, int bm, bool seg2, bool cs);   // 0, 3  
 gemm2_fn gemm2_pick_b(int tile, int am, int bm, bool seg2, bool cs);   // 1, 2   256x128, 128x256
 gemm2_fn gemm2_pick_c(int tile, int am, int bm, bool seg2, bool cs);   // 4, 5, 6, 9, 10  128x128, 128x64, 64x128
 gemm2_fn gemm2_pick_d(int tile, int am, int bm, bool seg2, bool cs);   // 7, 8   x160
-gemm2_fn gemm2_pick_ld(int tile, int am, int bm, int ldr);              // 0, 1, 4, 7, 8 with the fused down-projection
+gemm2_fn gemm2_pick_ld(int tile, int am, int bm, int ldr, int parts);   // 1, 4, 7, 8 with a fused LoRA projection
 
 // byte extent an operand's gathers may touch (the DMA descriptor's range)
 static long long operand_bytes(int mode, const bf16_t* p, long long ld, int MN, int K, const ConvGeom& g) {
@@ -44,7 +44,9 @@ int gemm2_launch(const GemmArgs& a, int tile, int splits, hipStream_t stream) {
   if (skinny4 && (tile == 5 || tile == 6) && !seg2) tile += 4;
   if (a.D) {   // LoRA down-projection fused (forward forms; split 1, whole adapter parts per tile: checked here)
     if (seg2 || cs || splits != 1 || a.batch > 1) return OTAMD_EUNSUPPORTED;
-    fn = gemm2_pick_ld(tile, a.amode, a.bmode, a.lora_r);
+    // the dgrad form over several adapter parts along K: K1 = rows per part (gemm.hip validates)
+    const int parts = (a.bmode == OPM_MN && a.K1 > 0 && a.K1 < a.K) ? a.K / a.K1 : 1;
+    fn = gemm2_pick_ld(tile, a.amode, a.bmode, a.lora_r, parts);
   } else switch (tile) {
     case 0: case 3: fn = gemm2_pick_a(tile, a.amode, a.bmode, seg2, cs); break;
     case 1: case 2: fn = gemm2_pick_b(tile, a.amode, a.bmode, seg2, cs); break;

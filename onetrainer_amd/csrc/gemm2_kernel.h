@@ -245,7 +245,10 @@ __device__ __forceinline__ int mn_chunk_off(int k, int c) {   // 16-byte chunk c
 // lora_pw = N): u = dY (sB) accumulated over the dgrad's K loop from D = (sB)^T [LDR][K], stored to T for the down
 // projection's weight gradient, and dX = dY W + u A with B2 = A^T [N][LDR] -- the u GEMM, its split-K reduce and the
 // second-segment DMA of the two-launch form (u GEMM + SEG2 dgrad) in one launch, bit-identical to it at one split.
-template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2, bool CS = false, int LDR = 0>
+// NPART > 1 (the dgrad form of a fused q|k|v site): the K range is NPART adapter parts of args.K1 rows each, u_p sums
+// over part p's rows only (u = dY (sB) with sB block-diagonal); one accumulator set per part, rotated at each part
+// boundary so the MFMAs always target set 0, and the second segment runs over all NPART * LDR columns of u.
+template <int AM, int BMODE, int BM, int BN, int NW, bool SEG2, int NS = 2, bool CS = false, int LDR = 0, int NPART = 1>
 __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && (BN == 128 || BN == 160)) ? 4 : NW / 4) gemm2_kernel(GemmArgs args, unsigned a_bytes, unsigned b_bytes,
                                                                  unsigned a2_bytes, unsigned b2_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -344,9 +347,12 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
   };
   // down-projection fusion: this wave's t blocks (rows i of its row range, its RCW column fragments of the part)
   constexpr int NBT1 = NBT > 0 ? NBT : 1, RCW1 = RCW > 0 ? RCW : 1;
-  float4v acc_t[NBT1];
+  static_assert(NPART == 1 || (LD && BMODE == OPM_MN), "multi-part u: the fused dgrad form only");
+  float4v acc_t[NPART][NBT1];   // [0]: the part of the current K step (earlier parts rotate towards NPART - 1)
 #pragma unroll
-  for (int b = 0; b < NBT1; ++b) acc_t[b] = float4v{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < NPART; ++q)
+#pragma unroll
+    for (int b = 0; b < NBT1; ++b) acc_t[q][b] = float4v{0.f, 0.f, 0.f, 0.f};
   bf16x8 ft0[RCW1], ft1[RCW1];
   auto load_t = [&](bf16x8 (&f)[RCW1], const char* it, int h) {
     if constexpr (LD) {
@@ -371,7 +377,7 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int c = 0; c < RCW; ++c)
-          acc_t[i * RCW + c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft[c], fa[i], acc_t[i * RCW + c], 0, 0, 0);
+          acc_t[0][i * RCW + c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft[c], fa[i], acc_t[0][i * RCW + c], 0, 0, 0);
     }
   };
   // the next half's fragment reads (h = 0, load_b then load_a order) with this wave's refill DMA pieces of the slot
@@ -553,6 +559,16 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
     const char* ia = smem + stg * STAGE;
     const char* ib = ia + ABYTES;
     const int nstg = stg + 1 == NS ? 0 : stg + 1;
+    if constexpr (NPART > 1) {   // tile kt opens a new adapter part (K1 = part rows, a multiple of 64)
+      if (kt > 0 && (kbeg + kt * 64) % args.K1 == 0) {
+#pragma unroll
+        for (int q = NPART - 1; q > 0; --q)
+#pragma unroll
+          for (int b = 0; b < NBT1; ++b) acc_t[q][b] = acc_t[q - 1][b];
+#pragma unroll
+        for (int b = 0; b < NBT1; ++b) acc_t[0][b] = float4v{0.f, 0.f, 0.f, 0.f};
+      }
+    }
     // phase A
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (OTAMD_GEMM_ABL != 3) {
@@ -606,7 +622,8 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
   }
 
   if constexpr (LD) {   // the second K segment from the t accumulated above (no split-K: the launcher checks)
-    constexpr int KS2 = (LDR + 31) / 32;
+    constexpr int LU = NPART * LDR;     // columns of t / u (all parts)
+    constexpr int KS2 = (LU + 31) / 32;
     const int g = lane >> 4;
     // up-projection fragments of this wave's output columns (K-mode rows of U, 16 bytes per lane), loaded before the t
     // hand-off so their latency hides behind it
@@ -618,32 +635,36 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
         const int n = n0 + wn * TN + j * 16 + (lane & 15);
         const int kk = 32 * s2 + 8 * g;
         fu[s2][j] = bf16x8{};
-        if (n < args.N && kk < LDR)
+        if (n < args.N && kk < LU)
           fu[s2][j] = *reinterpret_cast<const bf16x8*>(args.B2 + (long long)n * args.ldb2 + lpart * LDR + kk);
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     BARRIER();   // every wave is past its last stage read: stage 0 becomes the t image (BM rows x 64 k)
-    char* timg = smem;
+    // t / u image: columns [64 i, 64 i + 64) in stage i's A region (K-mode layout, as a DMA'd A tile)
+    static_assert((LU + 63) / 64 <= NS, "t / u columns must fit the ring's A regions");
     const bool t_out = (n0 % args.lora_pw) == 0;   // the part's first tile column stores t for the backward
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int q = 0; q < NPART; ++q)
 #pragma unroll
-      for (int c = 0; c < RCW; ++c) {
-        const float4v v = acc_t[i * RCW + c];
-        const int row = wm * TM + i * 16 + (lane & 15);
-        const int col = (wn * RCW + c) * 16 + 4 * g;
-        uint2 o;
-        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(timg + kimg_off(row, col >> 3) + (col & 7) * 2) = o;
-        const int m = m0 + row;
-        if (t_out && m < args.M) *reinterpret_cast<uint2*>(args.T + (long long)m * args.ldt + lpart * LDR + col) = o;
-      }
-    if constexpr (LDR % 32) {   // k in [LDR, 32 KS2): zeros (the up fragments there are zero; stale LDS bytes may be NaN)
-      constexpr int ZC = (32 - LDR % 32) / 8;   // 16-byte chunks per row
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int c = 0; c < RCW; ++c) {
+          const float4v v = acc_t[NPART - 1 - q][i * RCW + c];   // part q (the last part is in set 0)
+          const int row = wm * TM + i * 16 + (lane & 15);
+          const int col = q * LDR + (wn * RCW + c) * 16 + 4 * g;
+          uint2 o;
+          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          char* timg = smem + (col >> 6) * STAGE;
+          *reinterpret_cast<uint2*>(timg + kimg_off(row, (col & 63) >> 3) + (col & 7) * 2) = o;
+          const int m = m0 + row;
+          if (t_out && m < args.M) *reinterpret_cast<uint2*>(args.T + (long long)m * args.ldt + lpart * LDR + col) = o;
+        }
+    if constexpr (LU % 32) {   // k in [LU, 32 KS2): zeros (the up fragments there are zero; stale LDS bytes may be NaN)
+      constexpr int ZC = (32 - LU % 32) / 8;   // 16-byte chunks per row
       for (int e = threadIdx.x; e < BM * ZC; e += NW * 64) {
-        const int row = e / ZC, ch = LDR / 8 + e % ZC;
-        *reinterpret_cast<uint4*>(timg + kimg_off(row, ch)) = make_uint4(0u, 0u, 0u, 0u);
+        const int row = e / ZC, ch = (LU % 64) / 8 + e % ZC;
+        *reinterpret_cast<uint4*>(smem + (LU / 64) * STAGE + kimg_off(row, ch)) = make_uint4(0u, 0u, 0u, 0u);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -652,7 +673,7 @@ __global__ void __launch_bounds__(NW * 64, (LDR == 0 && NS == 2 && BM == 128 && 
     for (int s2 = 0; s2 < KS2; ++s2) {
       bf16x8 fa2[MI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) fa2[i] = frag_k2(timg, wm * TM + i * 16, 32 * s2);
+      for (int i = 0; i < MI; ++i) fa2[i] = frag_k2(smem + (s2 >> 1) * STAGE, wm * TM + i * 16, 32 * (s2 & 1));
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll

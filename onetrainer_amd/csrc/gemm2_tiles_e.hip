@@ -5,22 +5,26 @@
 #include "gemm2_kernel.h"
 
 template <int BM, int BN>
-static gemm2_fn pick_ld(int am, int bm, int ldr) {
+static gemm2_fn pick_ld(int am, int bm, int ldr, int parts) {
   if (ldr == 32) {
-    if (am == OPM_K && bm == OPM_K) return gemm2_kernel<OPM_K, OPM_K, BM, BN, 8, false, 2, false, 32>;
-    if (am == OPM_CONV_FWD && bm == OPM_K) return gemm2_kernel<OPM_CONV_FWD, OPM_K, BM, BN, 8, false, 2, false, 32>;
-    // the backward's input gradient with u = dY (sB) fused (MN-mode weights)
-    if (am == OPM_K && bm == OPM_MN) return gemm2_kernel<OPM_K, OPM_MN, BM, BN, 8, false, 2, false, 32>;
+    if (parts == 1) {
+      if (am == OPM_K && bm == OPM_K) return gemm2_kernel<OPM_K, OPM_K, BM, BN, 8, false, 2, false, 32>;
+      if (am == OPM_CONV_FWD && bm == OPM_K) return gemm2_kernel<OPM_CONV_FWD, OPM_K, BM, BN, 8, false, 2, false, 32>;
+      // the backward's input gradient with u = dY (sB) fused (MN-mode weights)
+      if (am == OPM_K && bm == OPM_MN) return gemm2_kernel<OPM_K, OPM_MN, BM, BN, 8, false, 2, false, 32>;
+    }
+    // ... of a fused q|k|v site: u over three K parts
+    if (parts == 3 && am == OPM_K && bm == OPM_MN) return gemm2_kernel<OPM_K, OPM_MN, BM, BN, 8, false, 2, false, 32, 3>;
   }
   return nullptr;
 }
 
-gemm2_fn gemm2_pick_ld(int tile, int am, int bm, int ldr) {
+gemm2_fn gemm2_pick_ld(int tile, int am, int bm, int ldr, int parts) {
   switch (tile) {
-    case 1: return pick_ld<256, 128>(am, bm, ldr);
-    case 4: return pick_ld<128, 128>(am, bm, ldr);
-    case 7: return pick_ld<128, 160>(am, bm, ldr);
-    case 8: return pick_ld<256, 160>(am, bm, ldr);
+    case 1: return pick_ld<256, 128>(am, bm, ldr, parts);
+    case 4: return pick_ld<128, 128>(am, bm, ldr, parts);
+    case 7: return pick_ld<128, 160>(am, bm, ldr, parts);
+    case 8: return pick_ld<256, 160>(am, bm, ldr, parts);
     default: return nullptr;
   }
 }

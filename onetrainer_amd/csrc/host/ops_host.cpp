@@ -311,12 +311,13 @@ std::atomic<long long> g_lora_dgrad_fused{0}, g_lora_dgrad_split{0};
 Tensor linear_dgrad_lora(const Tensor& dy, const Tensor& w, const Tensor& up2, const Tensor& down, const Tensor& upT,
                          const Tensor& downT, const Tensor& u_out, int64_t stream) {
   req(is_bf16(dy) && is_bf16(w) && dy.dim() == 2 && w.dim() == 2, "linear_dgrad_lora: bf16 2-D");
-  const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1), r = up2.size(1);
+  const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1), r = up2.size(1), r1 = upT.size(0);
   req(N == w.size(0) && N % 8 == 0 && K % 8 == 0 && aligned(dy) && aligned(w), "linear_dgrad_lora shapes");
   req(up2.dim() == 2 && up2.size(0) == N && down.dim() == 2 && down.size(0) == r && down.size(1) == K &&
-      upT.dim() == 2 && upT.size(0) == r && upT.size(1) == N && downT.dim() == 2 && downT.size(0) == K &&
+      upT.dim() == 2 && r1 > 0 && r % r1 == 0 && upT.size(1) == N && downT.dim() == 2 && downT.size(0) == K &&
       downT.size(1) == r && u_out.dim() == 2 && u_out.size(0) == M && u_out.size(1) == r, "linear_dgrad_lora: LoRA shapes");
-  if (lora_fuse_on() && lora_fuse_dgrad() && r == 32 && N % 64 == 0) {
+  const int64_t parts = r / r1;   // adapter parts along the dgrad's K (a fused q|k|v site: 3)
+  if (lora_fuse_on() && lora_fuse_dgrad() && r1 == 32 && (parts == 1 || parts == 3) && N % (64 * parts) == 0) {
     Tensor o = out2d({}, M, K, at::kBFloat16, dy);
     GemmArgs a = new_args();
     a.A = dy.data_ptr(); a.lda = ld_rows(dy); a.amode = OPM_K;
@@ -337,7 +338,8 @@ Tensor linear_dgrad_lora(const Tensor& dy, const Tensor& w, const Tensor& up2, c
       a.D = upT.data_ptr(); a.ldd = ld_rows(upT);
       a.B2 = downT.data_ptr(); a.ldb2 = ld_rows(downT);
       a.T = u_out.data_ptr(); a.ldt = ld_rows(u_out);
-      a.lora_r = (int)r; a.lora_pw = (int)K;
+      a.lora_r = (int)r1; a.lora_pw = (int)K;
+      a.K1 = parts > 1 ? (int)(N / parts) : 0;
       const int rc = otamd_gemm_explicit(&a, tile, 1, nullptr, 0, S(stream));
       if (rc != OTAMD_EUNSUPPORTED) {
         check(rc, "otamd_gemm_explicit (LoRA dgrad fused)");

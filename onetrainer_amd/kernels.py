@@ -582,9 +582,10 @@ _LORA_FUSE_DGRAD = os.environ.get("OTAMD_LORA_FUSE_DGRAD", "1") != "0"
 
 def linear_dgrad_lora(dy: torch.Tensor, w: torch.Tensor, up2: torch.Tensor, down: torch.Tensor, upT: torch.Tensor,
                       downT: torch.Tensor, u_out: torch.Tensor, tile=None) -> torch.Tensor:
-    """LoRA backward input gradient of a frozen single-module Linear (LoRAModule.forward differentiated,
-    modules/module/LoRAModule.py:318-322): dx = dy w + u down with u = dy up2 (alpha/rank folded into up2) written to
-    u_out [M, r] for the down projection's weight gradient.  One launch with u accumulated inside the dgrad GEMM's K
+    """LoRA backward input gradient of a frozen Linear (LoRAModule.forward differentiated,
+    modules/module/LoRAModule.py:318-322): dx = dy w + u down with u = dy up2 (alpha/rank folded into up2, block-
+    diagonal over a fused group's parts) written to u_out [M, P r] for the down projections' weight gradient; upT =
+    [r, N] (the parts' ups transposed side by side), downT = down^T [K, P r].  One launch with u accumulated inside the dgrad GEMM's K
     loop (GemmArgs.D = upT = up2^T, B2 = downT = down^T) when the two-launch form's plan allows, else u, then the
     dgrad with u as its second K segment; bit-identical either way at one split (ops_host.cpp linear_dgrad_lora).
     tile: force the tile (tests)."""
@@ -594,11 +595,13 @@ def linear_dgrad_lora(dy: torch.Tensor, w: torch.Tensor, up2: torch.Tensor, down
     _req(dy.dtype == BF16 and w.dtype == BF16 and dy.dim() == 2 and w.dim() == 2, "linear_dgrad_lora: bf16 2-D")
     M, N = dy.shape
     Kd = w.shape[1]
-    r = up2.shape[1]
+    r, r1 = up2.shape[1], upT.shape[0]
     _req(w.shape[0] == N and N % 8 == 0 and Kd % 8 == 0 and _aligned(dy) and _aligned(w), "linear_dgrad_lora shapes")
-    _req(tuple(up2.shape) == (N, r) and tuple(down.shape) == (r, Kd) and tuple(upT.shape) == (r, N)
-         and tuple(downT.shape) == (Kd, r) and tuple(u_out.shape) == (M, r), "linear_dgrad_lora: LoRA shapes")
-    if _LORA_FUSE["on"] and _LORA_FUSE_DGRAD and r == 32 and N % 64 == 0:
+    _req(r1 > 0 and r % r1 == 0 and tuple(up2.shape) == (N, r) and tuple(down.shape) == (r, Kd)
+         and tuple(upT.shape) == (r1, N) and tuple(downT.shape) == (Kd, r) and tuple(u_out.shape) == (M, r),
+         "linear_dgrad_lora: LoRA shapes")
+    parts = r // r1   # adapter parts along the dgrad's K (a fused q|k|v site: 3)
+    if _LORA_FUSE["on"] and _LORA_FUSE_DGRAD and r1 == 32 and parts in (1, 3) and N % (64 * parts) == 0:
         out = torch.empty((M, Kd), dtype=BF16, device=dy.device)
         a = _new_args()
         a.A, a.lda, a.amode = _p(dy), _ld_rows(dy), OPM_K
@@ -622,7 +625,8 @@ def linear_dgrad_lora(dy: torch.Tensor, w: torch.Tensor, up2: torch.Tensor, down
             a.D, a.ldd = _p(upT), _ld_rows(upT)
             a.B2, a.ldb2 = _p(downT), _ld_rows(downT)
             a.T, a.ldt = _p(u_out), _ld_rows(u_out)
-            a.lora_r, a.lora_pw = r, Kd
+            a.lora_r, a.lora_pw = r1, Kd
+            a.K1 = N // parts if parts > 1 else 0
             rc = lib().otamd_gemm_explicit(C.byref(a), tile, 1, None, 0, stream_handle())
             if rc != 3:   # OTAMD_EUNSUPPORTED: no fused instance for this tile / width
                 check(rc, "otamd_gemm_explicit (LoRA dgrad fused)")

@@ -177,8 +177,8 @@ class LoraLinearFn(torch.autograd.Function):
     """y = x W^T (+b) (+residual) + s * (x A^T) B^T with a frozen base (LoRAModule.forward,
     modules/module/LoRAModule.py:318-322).  Forward: one launch with t = x A^T accumulated in the base GEMM's K loop
     and [t | s B] as its second K segment (kernels.linear_lora; two launches where the plan does not allow it).
-    Backward: u = dy (sB); dx = [dy | u] [W ; A] (one GEMM; on single-module sites u is accumulated inside it,
-    kernels.linear_dgrad_lora); dA = u^T x; dB_p = s dy_p^T t_p per fused part; all adapter grads fp32."""
+    Backward: u = dy (sB); dx = [dy | u] [W ; A] (one GEMM; at r = 32 on single-module and q|k|v sites u is
+    accumulated inside it, kernels.linear_dgrad_lora); dA = u^T x; dB_p = s dy_p^T t_p per fused part; all adapter grads fp32."""
 
     @staticmethod
     def forward(ctx, x, wref, bref, residual, site, *params):
@@ -225,7 +225,7 @@ class LoraLinearFn(torch.autograd.Function):
                 dy2 = dy2.contiguous()
             if need_dx and site.upT is not None:
                 # one launch: u = dy (sB) inside the input-gradient GEMM's K loop (kernels.linear_dgrad_lora)
-                u = torch.empty((dy2.shape[0], site.rank), dtype=dy2.dtype, device=dy2.device)
+                u = torch.empty((dy2.shape[0], site.up2.shape[1]), dtype=dy2.dtype, device=dy2.device)
                 dx = K.linear_dgrad_lora(dy2, wref.w, site.up2, site.down, site.upT, site.downT, u).view(ctx.xshape)
                 with S.wgrad_region((dy2, x2, t, u)):
                     wgrads(dy2, u)

@@ -51,9 +51,10 @@ class LoraSite:
     n_total: int = 0         # fused GEMM output width
     down: torch.Tensor | None = None     # bf16 shadow [P*r, cin] or [r, k, k, cin]
     up2: torch.Tensor | None = None      # bf16 shadow [n_total, P*r] (block-diagonal, zero rows elsewhere), x alpha/r
-    upT: torch.Tensor | None = None      # bf16 shadow [r, n_total] = up2^T, and downT [cin, r] = down^T: the operands of
-    downT: torch.Tensor | None = None    # the fused backward input gradient (kernels.linear_dgrad_lora); single-module
-    #                                      linear sites at r = 32 only (the instances), else None
+    upT: torch.Tensor | None = None      # bf16 shadow [r, n_total] = the parts' (s up_p)^T side by side, and downT
+    downT: torch.Tensor | None = None    # [cin, P r] = down^T: the operands of the fused backward input gradient
+    #                                      (kernels.linear_dgrad_lora); linear sites at r = 32 with one module or a
+    #                                      fully adapted q|k|v group (the instances), else None
     g_down: torch.Tensor | None = None   # fp32 grad view, shape of `down`
     g_up: list = field(default_factory=list)   # fp32 grad views [cout_p, r]
     store: FlatParamStore | None = None
@@ -173,9 +174,10 @@ class LoRAWrapper:
             uoff = (doff + dn + 7) // 8 * 8
             total = uoff + un
             toff = None
-            if s.kind == "linear" and len(s.group) == 1 and P == 1 and rank == 32:
-                toff = (total + 7) // 8 * 8                  # upT [r, n_total], then downT [cin, r]
-                total = toff + rank * s.n_total + s.cin * rank
+            if s.kind == "linear" and rank == 32 and ((P == 1 and len(s.group) == 1) or
+                                                      (P == 3 and len(s.group) == 3 and s.part_width > 0)):
+                toff = (total + 7) // 8 * 8                  # upT [r, n_total], then downT [cin, P r]
+                total = toff + rank * s.n_total + s.cin * P * rank
             layout.append((doff, uoff, toff))
         self.shadow = torch.zeros(total + 8, dtype=torch.bfloat16, device=model.device)
         entries = []
@@ -196,12 +198,14 @@ class LoRAWrapper:
                 us = self.store.slots[s.names[P + p]]
                 entries.append((us.offset, uoff + s.ranges[p][0] * P * rank + p * rank, s.couts[p], rank, P * rank,
                                 self.scale))
-            if toff is not None:
+            if toff is not None:   # upT = [(s up_0)^T | (s up_1)^T | ...] along the output, downT = [down_0; ...]^T
                 s.upT = self.shadow[toff:toff + rank * s.n_total].view(rank, s.n_total)
-                s.downT = self.shadow[toff + rank * s.n_total:toff + rank * s.n_total + s.cin * rank].view(s.cin, rank)
-                us = self.store.slots[s.names[1]]
-                entries.append((us.offset, toff, s.n_total, rank, s.n_total, self.scale, 1))   # (s up)^T
-                entries.append((dslot.offset, toff + rank * s.n_total, rank, s.cin, rank, 1.0, 1))   # down^T
+                e0 = toff + rank * s.n_total
+                s.downT = self.shadow[e0:e0 + s.cin * P * rank].view(s.cin, P * rank)
+                for p in range(P):
+                    us = self.store.slots[s.names[P + p]]
+                    entries.append((us.offset, toff + s.ranges[p][0], s.couts[p], rank, s.n_total, self.scale, 1))
+                entries.append((dslot.offset, e0, P * rank, s.cin, P * rank, 1.0, 1))
         arr = (_lib.LoraShadowEntry * len(entries))()
         for i, (src, dst, rows, cols, ld, sc, *tr) in enumerate(entries):
             arr[i].src, arr[i].dst, arr[i].rows, arr[i].cols, arr[i].dst_ld, arr[i].scale = src, dst, rows, cols, ld, sc

@@ -183,11 +183,39 @@ def test_lora_shadow_transposes(dev):
     lw.store.data.copy_(torch.randn(lw.store.data.shape, generator=g, device=dev) * 0.1)
     lw.refresh()
     n = 0
+    nq = 0
     for s in lw.sites:
         if s.upT is None:
-            assert s.kind != "linear" or len(s.group) > 1
+            assert s.kind != "linear" or len(s.group) not in (1, 3), s.key
             continue
+        P, r = len(s.modules), 32
         n += 1
-        assert torch.equal(s.upT, s.up2.t()), s.key
+        nq += P == 3
+        want = torch.cat([s.up2[p * s.part_width:(p + 1) * s.part_width, p * r:(p + 1) * r].t() for p in range(P)], 1)
+        assert torch.equal(s.upT, want), s.key
         assert torch.equal(s.downT, s.down.t()), s.key
-    assert n > 0
+    assert n > 0 and nq > 0
+
+
+@pytest.mark.parametrize("tile", [1, 4, 7, 8])
+@pytest.mark.parametrize("M,pw,Kin", [(4096, 1280, 1280), (1000, 640, 640)])
+def test_linear_dgrad_lora_fused_qkv_bitwise(dev, monkeypatch, tile, M, pw, Kin):
+    """the fused q|k|v site's input gradient: three adapter parts along the dgrad's K (u_p sums over part p's rows,
+    rotating accumulators), against the two-launch form with the block-diagonal up at one split: bit-identical."""
+    if Kin % BN[tile]:
+        pytest.skip("input width not a tile multiple: the launcher refuses (two-launch form)")
+    torch.manual_seed(26)
+    r, P = 32, 3
+    dy, w = rnd(M, P * pw, dev=dev), rnd(P * pw, Kin, dev=dev, scale=0.05)
+    up2, down = block_up(P, pw, r, dev), rnd(P * r, Kin, dev=dev, scale=0.05)
+    upT = torch.cat([up2[p * pw:(p + 1) * pw, p * r:(p + 1) * r].t() for p in range(P)], dim=1).contiguous()
+    downT = down.t().contiguous()
+    u = torch.full((M, P * r), float("nan"), device=dev, dtype=BF)
+    dx = K.linear_dgrad_lora(dy, w, up2, down, upT, downT, u, tile=tile)
+
+    def ref():
+        u_ref = K.linear_dgrad(dy, up2)
+        return u_ref, K.linear_dgrad(dy, w, lora=(u_ref, down))
+    u_ref, dx_ref = two_launch_split1(monkeypatch, ref)
+    assert torch.equal(u, u_ref), (u.float() - u_ref.float()).abs().max().item()
+    assert torch.equal(dx, dx_ref), (dx.float() - dx_ref.float()).abs().max().item()

@@ -1,4 +1,4 @@
-# Round 6: LoRA backward input gradient with u = dy (sB) fused into the dgrad GEMM -- fused-LoRA GPU tests, LoRA /
+# Round 6: LoRA backward input gradient with u = dy (sB) fused into the dgrad GEMM (single-module and q|k|v sites) -- fused-LoRA GPU tests, LoRA /
 # hazard tests, the full-width SDXL LoRA oracle test, then C4 with OTAMD_LORA_FUSE_DGRAD=1 vs 0 interleaved
 set -o pipefail
 export TMPDIR=/tmp; mkdir -p gpurun_out
