@@ -333,7 +333,8 @@ def main():
     ms1 = torch.cuda.memory_stats(dev)
     alloc = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries",
                                                           "num_sync_all_streams")}
-    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    step_ms_seq = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    step_ms = sorted(step_ms_seq)
     p50 = step_ms[len(step_ms) // 2]
     p90 = step_ms[min(len(step_ms) - 1, int(0.9 * len(step_ms)))]
     loss_last = torch.stack(losses).float().mean()
@@ -407,6 +408,8 @@ def main():
         "step_ms_p50": round(p50, 2),
         "step_ms_p90": round(p90, 2),
         "step_ms_max": round(step_ms[-1], 2),
+        "step_ms_each": [round(t, 2) for t in step_ms_seq],   # timed steps in order
+        "step_buckets": [list(b) for b in order[args.warmup:args.warmup + args.steps]] if sdxl_lora else None,
         "allocator_in_timed_steps": alloc,
         "higher_is_better": True,
         "scaling": "weak",

@@ -13,6 +13,7 @@
 #include <torch/extension.h>
 
 #include <array>
+#include <map>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -227,6 +228,36 @@ bool lora_fuse_conv() {
   return v;
 }
 
+// measured fused-LoRA choices (kernels._lora_plans, lora_plans_mi355x.json): (form, N, K, parts, M class) -> tile,
+// or -1 for the two launches; shapes without an entry follow the two-launch form's plan
+std::shared_mutex g_lora_plans_mu;
+std::map<std::array<int64_t, 5>, int> g_lora_plans;
+void set_lora_plans(const std::vector<std::vector<int64_t>>& rows) {
+  std::unique_lock<std::shared_mutex> lk(g_lora_plans_mu);
+  g_lora_plans.clear();
+  for (const auto& r : rows) {
+    req(r.size() == 6, "lora plan row: form, N, K, parts, mclass, tile");
+    g_lora_plans[{r[0], r[1], r[2], r[3], r[4]}] = (int)r[5];
+  }
+}
+// The entries were measured at M = 4096 / 16384 (one tile per CU or whole waves of them); at the aspect buckets' other
+// row counts a tile grid just past a multiple of the 256 CUs runs a second round for a few tiles (4160 rows on
+// 128x160 tiles: 264 tiles, ~2x the time), so an entry applies only while the grid fills its rounds >= 85 %.
+int lora_plan(int64_t form, int64_t N, int64_t K, int64_t parts, int64_t M) {
+  int tile = 0;
+  {
+    std::shared_lock<std::shared_mutex> lk(g_lora_plans_mu);
+    auto it = g_lora_plans.find({form, N, K, parts, M >= 8192 ? 1 : 0});
+    if (it == g_lora_plans.end()) return 0;
+    tile = it->second;
+  }
+  if (tile <= 0) return tile;
+  const int64_t bm = (tile == 1 || tile == 8) ? 256 : 128, bn = (tile == 7 || tile == 8) ? 160 : 128;
+  const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  const int64_t rounds = (tiles + 255) / 256;
+  return tiles * 100 >= rounds * 256 * 85 ? tile : 0;
+}
+
 bool lora_down_fused(GemmArgs& a, const Tensor& down2d, const Tensor& up2, const Tensor& t2d, int64_t k1, int64_t r,
                      int64_t pw, int64_t stream) {
   if (!lora_fuse_on() || r != 32 || pw <= 0 || a.N % pw || k1 % 64) return false;
@@ -234,7 +265,12 @@ bool lora_down_fused(GemmArgs& a, const Tensor& down2d, const Tensor& up2, const
   GemmArgs k = a;   // the two-launch form's base GEMM signature (plan table key)
   if (!seg2(k, t2d, up2, k1, false)) return false;
   int tile = 0, splits = 0;
-  if (!lookup_plan(tune_key(k), tile, splits)) {
+  const int lp = a.amode == OPM_K ? lora_plan(0, a.N, k1, a.N / pw, a.M) : 0;
+  if (lp == -1) return false;
+  if (lp > 0) {
+    tile = lp;
+    splits = 1;
+  } else if (!lookup_plan(tune_key(k), tile, splits)) {
     tile = otamd_gemm_plan_tile(&k, 0);
     if (otamd_gemm_plan(&k, 0, &splits) < 0) return false;
   }
@@ -327,7 +363,11 @@ Tensor linear_dgrad_lora(const Tensor& dy, const Tensor& w, const Tensor& up2, c
     GemmArgs k = a;   // the two-launch form's dgrad signature (plan table key)
     req(seg2(k, u_out, down, N, true), "linear_dgrad_lora: second segment");
     int tile = 0, splits = 0;
-    if (!lookup_plan(tune_key(k), tile, splits)) {
+    const int lp = lora_plan(1, K, N, parts, M);
+    if (lp > 0) {
+      tile = lp;
+      splits = 1;
+    } else if (lp == 0 && !lookup_plan(tune_key(k), tile, splits)) {
       tile = otamd_gemm_plan_tile(&k, 0);
       if (otamd_gemm_plan(&k, 0, &splits) < 0) splits = 0;
     }
@@ -716,6 +756,7 @@ PYBIND11_MODULE(_otamd_host, m) {
   m.def("conv2d", &conv2d);
   m.def("linear_lora", &linear_lora);
   m.def("linear_dgrad_lora", &linear_dgrad_lora);
+  m.def("set_lora_plans", &set_lora_plans);
   m.def("lora_dgrad_fused_counts",
         []() { return std::make_pair((long long)g_lora_dgrad_fused, (long long)g_lora_dgrad_split); });
   m.def("conv2d_lora", &conv2d_lora);

@@ -337,6 +337,7 @@ def _host():
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
             mod.set_plan_table([list(k) + [t, sp] for k, (t, sp) in _plan_table().items()])
+            mod.set_lora_plans([list(k) + [t] for k, t in _lora_plans().items()])
             import atexit
             atexit.register(mod.clear_workspaces)   # free the cached workspaces while the allocator still exists
             _HOST["mod"] = mod
@@ -473,6 +474,33 @@ def set_lora_fuse(on: bool) -> None:
         h.set_lora_fuse(bool(on))
 
 
+_LORA_PLANS: dict = {}
+
+
+def _lora_plans() -> dict:
+    """(form, N, K, parts, M class) -> fused tile or -1 (two launches): lora_plans_mi355x.json (OTAMD_LORA_PLANS=0:
+    none, the two-launch form's plan decides -- the A/B reference)"""
+    if not _LORA_PLANS and os.environ.get("OTAMD_LORA_PLANS", "1") != "0":
+        import json
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lora_plans_mi355x.json")
+        with open(path) as f:
+            for e in json.load(f)["plans"]:
+                if e["tile"] > 0 or os.environ.get("OTAMD_LORA_PLANS", "1") != "2":   # =2: fused tiles only
+                    _LORA_PLANS[(e["form"], e["N"], e["K"], e["parts"], e["mclass"])] = e["tile"]
+    return _LORA_PLANS
+
+
+def _lora_plan(form: int, N: int, K: int, parts: int, M: int):
+    """as ops_host.cpp lora_plan: a tile entry applies only while its grid fills its rounds of 256 CUs >= 85 %"""
+    tile = _lora_plans().get((form, N, K, parts, int(M >= 8192)))
+    if not tile or tile < 0:
+        return tile
+    bm, bn = (256 if tile in (1, 8) else 128), (160 if tile in (7, 8) else 128)
+    tiles = -(-M // bm) * -(-N // bn)
+    rounds = -(-tiles // 256)
+    return tile if tiles * 100 >= rounds * 256 * 85 else None
+
+
 def _lora_down_fused(a: GemmArgs, down2d, up2, t2d, k1: int, r: int, pw: int, device, tile=None) -> bool:
     """one launch computing t = A down^T (into t2d) and y = A B^T + t up2^T (GemmArgs.D); False when the plan of the
     two-launch form's base GEMM is not a one-split launch on a tile with a fused instance (ops_host.cpp
@@ -484,6 +512,11 @@ def _lora_down_fused(a: GemmArgs, down2d, up2, t2d, k1: int, r: int, pw: int, de
     k = GemmArgs.from_buffer_copy(a)
     if not _seg2(k, t2d, up2, k1, False):
         return False
+    lp = _lora_plan(0, a.N, k1, a.N // pw, a.M) if tile is None and a.amode == OPM_K else None
+    if lp == -1:
+        return False
+    if lp:
+        tile = lp
     if tile is None:
         plan = _plan_table().get(_tune_key(k))
         if plan is None:
@@ -611,7 +644,12 @@ def linear_dgrad_lora(dy: torch.Tensor, w: torch.Tensor, up2: torch.Tensor, down
         k = GemmArgs.from_buffer_copy(a)
         _req(_seg2(k, u_out, down, N, True), "linear_dgrad_lora: second segment")
         splits = 1
-        if tile is None:
+        lp = _lora_plan(1, Kd, N, parts, M) if tile is None else None
+        if lp == -1:
+            splits = 0
+        elif lp:
+            tile = lp
+        if tile is None and lp != -1:
             plan = _plan_table().get(_tune_key(k))
             if plan is None:
                 s_out = C.c_int(0)

@@ -21,8 +21,9 @@ TILES = {1: 128, 4: 128, 7: 160, 8: 160}   # fused tiles -> BN
 # ff.proj, ff.net.2, proj_in / proj_out)
 FWD = [(4096, 1280, 3840, 3), (4096, 1280, 1280, 1), (4096, 1280, 10240, 1), (4096, 5120, 1280, 1),
        (16384, 640, 1920, 3), (16384, 640, 640, 1), (16384, 640, 5120, 1), (16384, 2560, 640, 1)]
-DGRAD = [(4096, 1280, 1280), (4096, 10240, 1280), (4096, 1280, 5120), (16384, 640, 640), (16384, 5120, 640),
-         (16384, 640, 2560)]   # (M, N out = dgrad K, K in = dgrad N)
+DGRAD = [(4096, 1280, 1280, 1), (4096, 10240, 1280, 1), (4096, 1280, 5120, 1), (16384, 640, 640, 1),
+         (16384, 5120, 640, 1), (16384, 640, 2560, 1), (4096, 3840, 1280, 3), (16384, 1920, 640, 3)]
+# (M, N out = dgrad K, K in = dgrad N, parts along K)
 
 
 def timeit(f, reps):
@@ -60,17 +61,25 @@ def main():
         t = torch.empty(M, P * r, device=dev, dtype=BF)
         res = {"form": "fwd", "M": M, "K": Kd, "N": N, "parts": P,
                "planned_us": timeit(lambda: K.linear_lora(x, w, None, None, down, up2, t, r, pw), a.reps)}
+        K.set_lora_fuse(False)
+        res["two_launch_us"] = timeit(lambda: K.linear_lora(x, w, None, None, down, up2, t, r, pw), a.reps)
+        K.set_lora_fuse(True)
         for tile, bn in TILES.items():
             if pw % bn == 0:
                 res[f"tile{tile}_us"] = timeit(lambda: K.linear_lora(x, w, None, None, down, up2, t, r, pw, tile=tile),
                                                a.reps)
         print(json.dumps(res), flush=True)
-    for M, Nout, Kin in DGRAD:
+    for M, Nout, Kin, P in DGRAD:
+        pw = Nout // P
         dy, w = rnd(M, Nout), rnd(Nout, Kin, scale=0.05)
-        up2, down = rnd(Nout, r, scale=0.05), rnd(r, Kin, scale=0.05)
-        upT, downT = up2.t().contiguous(), down.t().contiguous()
-        u = torch.empty(M, r, device=dev, dtype=BF)
-        res = {"form": "dgrad", "M": M, "N_out": Nout, "K_in": Kin,
+        up2 = torch.zeros(Nout, P * r, device=dev, dtype=BF)
+        for p in range(P):
+            up2[p * pw:(p + 1) * pw, p * r:(p + 1) * r] = rnd(pw, r, scale=0.05)
+        down = rnd(P * r, Kin, scale=0.05)
+        upT = torch.cat([up2[p * pw:(p + 1) * pw, p * r:(p + 1) * r].t() for p in range(P)], 1).contiguous()
+        downT = down.t().contiguous()
+        u = torch.empty(M, P * r, device=dev, dtype=BF)
+        res = {"form": "dgrad", "M": M, "N_out": Nout, "K_in": Kin, "parts": P,
                "planned_us": timeit(lambda: K.linear_dgrad_lora(dy, w, up2, down, upT, downT, u), a.reps)}
         K.set_lora_fuse(False)
         res["two_launch_us"] = timeit(lambda: K.linear_dgrad_lora(dy, w, up2, down, upT, downT, u), a.reps)
