@@ -185,6 +185,12 @@ int otamd_adaln_bwd_res(const void* x, long long ldx, const void* dy, long long 
                         int scale_off, int B, const float* mean, const float* rstd, void* dmod, float* part,
                         hipStream_t s);
 
+/* replaces: the modulation half of that autograd alone (bf16 d(shift), d(scale) into dmod), for a caller that runs it
+   beside the dx pass on the weight-gradient stream (the modulation only feeds weight gradients) */
+int otamd_adaln_dmod(const void* x, long long ldx, const void* dy, long long lddy, int rows, int D, long long ldm,
+                     int shift_off, int scale_off, int B, const float* mean, const float* rstd, void* dmod, float* part,
+                     hipStream_t s);
+
 /* scratch floats the adaLN / gated-add backward reductions need */
 long long otamd_mod_part_floats(int T, int D, int B);
 

@@ -151,6 +151,7 @@ SIGNATURES: dict[str, list] = {
     "otamd_adaln_fwd": [VP, LL, VP, LL, I, I, F, VP, LL, I, I, I, VP, VP, VP],
     "otamd_adaln_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, LL, I, I, I, VP, VP, VP, VP, VP],
     "otamd_adaln_bwd_res": [VP, LL, VP, LL, VP, LL, VP, LL, I, I, VP, LL, I, I, I, VP, VP, VP, VP, VP],
+    "otamd_adaln_dmod": [VP, LL, VP, LL, I, I, LL, I, I, I, VP, VP, VP, VP, VP],
     "otamd_mod_part_floats": [I, I, I],
     "otamd_gated_add_fwd": [VP, LL, VP, LL, VP, LL, I, I, VP, LL, I, I, VP],
     "otamd_gated_add_bwd": [VP, LL, VP, LL, VP, LL, I, I, VP, LL, I, I, VP, VP, VP],

@@ -474,6 +474,25 @@ static int adaln_bwd_impl(const void* x, long long ldx, const void* dy, long lon
   return OTAMD_OK;
 }
 
+// the modulation gradient alone (the dmod half of otamd_adaln_bwd): dmod[b, shift_off + c] = sum_t dy,
+// dmod[b, scale_off + c] = sum_t dy * xhat -- queued on the weight-gradient stream when the modulation branch runs
+// there (module/flux.py), while the dx pass stays on the critical stream
+OTAMD_API int otamd_adaln_dmod(const void* x, long long ldx, const void* dy, long long lddy, int rows, int D, long long ldm,
+                               int shift_off, int scale_off, int B, const float* mean, const float* rstd, void* dmod,
+                               float* part, hipStream_t s) {
+  if (!x || !dy || !dmod || !part || !mean || !rstd || rows <= 0 || B <= 0 || rows % B || D % 8 || ldx % 8 ||
+      lddy % 8 || ldm % 8 || !a16(x) || !a16(dy))
+    return OTAMD_EINVAL;
+  const int T = rows / B, S = mod_splits(T, D, B);
+  dim3 g((D / 8 + 255) / 256, B, S);
+  mod_partial_kernel<0><<<g, 256, 0, s>>>((const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, T, D, B, (T + S - 1) / S,
+                                          mean, rstd, nullptr, 0, 0, nullptr, 0, part);
+  OTAMD_CHECK_LAUNCH();
+  mod_reduce_kernel<<<gfor(2LL * B * D), 256, 0, s>>>(part, S, B, 2, D, (bf16_t*)dmod, ldm, scale_off, shift_off);
+  OTAMD_CHECK_LAUNCH();
+  return OTAMD_OK;
+}
+
 OTAMD_API int otamd_adaln_bwd(const void* x, long long ldx, const void* dy, long long lddy, void* dx, long long lddx,
                               int rows, int D, const void* mod, long long ldm, int shift_off, int scale_off, int B,
                               const float* mean, const float* rstd, void* dmod, float* part, hipStream_t s) {

@@ -1569,6 +1569,18 @@ def adaln_bwd(x, dy, mod, shift_off, scale_off, B, stats, dmod=None, dx=None, dr
     return dx
 
 
+def adaln_dmod(x, dy, mod, shift_off, scale_off, B, stats, dmod):
+    """the adaLN's modulation gradient alone (d shift, d scale into dmod), e.g. on the weight-gradient stream"""
+    rows, D, ldx = _rows2d(x)
+    _, _, lddy = _rows2d(dy)
+    _mod_ok(mod, B, shift_off, scale_off)
+    _req(dmod.shape == mod.shape and dmod.stride() == mod.stride(), "dmod like mod")
+    part = _mod_part(rows // B, D, B, x.device)
+    mean, rstd = stats
+    check(lib().otamd_adaln_dmod(_p(x), ldx, _p(dy), lddy, rows, D, mod.stride(0), shift_off, scale_off, B, _p(mean),
+                                 _p(rstd), _p(dmod), _p(part), stream_handle()), "otamd_adaln_dmod")
+
+
 def gated_add_fwd(x, y, mod, gate_off, B, out=None):
     rows, D, ldx = _rows2d(x)
     _, _, ldy = _rows2d(y)

@@ -15,6 +15,7 @@ MI355X layout (not a translation of the diffusers module tree):
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass
@@ -24,6 +25,7 @@ import torch
 
 from .. import kernels as K
 from . import functional as Fn
+from . import streams as S
 from . import flux_ops as O
 from .param_store import FlatParamStore
 
@@ -52,6 +54,9 @@ class FluxConfig:
 # the blocks' adaLN inputs are also their residuals: AdaLNResFn sums the two gradient contributions inside the adaLN
 # backward (OTAMD_ADALN_RES=0: autograd adds them, the A/B reference)
 _ADALN_RES = os.environ.get("OTAMD_ADALN_RES", "1") != "0"
+# the embedders, the modulation GEMMs and the adaLN modulation sums on the weight-gradient stream (FluxTransformer.forward;
+# OTAMD_MOD_SIDE=0: on the current stream, the A/B reference)
+_MOD_SIDE = os.environ.get("OTAMD_MOD_SIDE", "1") != "0"
 
 
 def _adaln_res(hx, emb, st, segs, B):
@@ -279,6 +284,20 @@ class FluxTransformer2DModel:
             out[m] = (emb, O.ModState(emb), 0)
         return out
 
+    def _embed_and_modulate(self, t_eff, g_eff, pooled_b):
+        """time / guidance / pooled-text embedders -> silu(temb) -> every modulation GEMM (see _modulation)"""
+        te = "time_text_embed."
+        temb = self._linear(Fn.SiLUFn.apply(self._linear(K.timestep_embedding(t_eff, 256),
+                                                         te + "timestep_embedder.linear_1")),
+                            te + "timestep_embedder.linear_2")
+        if g_eff is not None:
+            temb = self._linear(Fn.SiLUFn.apply(self._linear(K.timestep_embedding(g_eff, 256),
+                                                             te + "guidance_embedder.linear_1")),
+                                te + "guidance_embedder.linear_2", residual=temb)
+        temb = self._linear(Fn.SiLUFn.apply(self._linear(pooled_b, te + "text_embedder.linear_1")),
+                            te + "text_embedder.linear_2", residual=temb)
+        return self._modulation(Fn.SiLUFn.apply(temb))
+
     def forward(self, tokens, timestep, guidance, pooled, ehs, h, w):
         """tokens: packed image latents [N*B, in_channels] bf16, rows t*B + b (K.flux_pack);
         timestep: [B] fp32 = the reference's t / 1000; guidance [B] fp32 or None; pooled [B, P] bf16;
@@ -288,21 +307,29 @@ class FluxTransformer2DModel:
         B, L, _ = ehs.shape
         N = (h // 2) * (w // 2)
         T = L + N
-        te = "time_text_embed."
         # diffusers: timestep.to(bf16) * 1000 in bf16, then the fp32 sinusoid (BaseFluxSetup passes t / 1000)
         t_eff = (timestep.to(BF16) * 1000).float().contiguous()
-        temb = self._linear(Fn.SiLUFn.apply(self._linear(K.timestep_embedding(t_eff, 256),
-                                                         te + "timestep_embedder.linear_1")),
-                            te + "timestep_embedder.linear_2")
-        if cfg.guidance_embeds:
-            g_eff = (guidance.to(BF16) * 1000).float().contiguous()
-            temb = self._linear(Fn.SiLUFn.apply(self._linear(K.timestep_embedding(g_eff, 256),
-                                                             te + "guidance_embedder.linear_1")),
-                                te + "guidance_embedder.linear_2", residual=temb)
-        temb = self._linear(Fn.SiLUFn.apply(self._linear(pooled.to(BF16).contiguous(), te + "text_embedder.linear_1")),
-                            te + "text_embedder.linear_2", residual=temb)
-        semb = Fn.SiLUFn.apply(temb)
-        mod = self._modulation(semb)
+        g_eff = (guidance.to(BF16) * 1000).float().contiguous() if cfg.guidance_embeds else None
+        pooled_b = pooled.to(BF16).contiguous()
+        # The embedders and every modulation GEMM run on the weight-gradient stream: their autograd nodes then run their
+        # backward there too (torch runs a node's backward on its forward stream and orders the streams at each edge)
+        # -- that branch only feeds weight gradients -- and the adaLN modulation sums follow (flux_ops._dmod_side).
+        # (Not while a step graph is captured.)
+        side = S.side_stream() if _MOD_SIDE and not torch.cuda.is_current_stream_capturing() else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            mod = self._embed_and_modulate(t_eff, g_eff, pooled_b)
+        if side is not None:
+            for u in (t_eff, g_eff, pooled_b):
+                if u is not None:
+                    u.record_stream(side)
+            S.join()   # the blocks read the modulation vectors
+            main = torch.cuda.current_stream()
+            for emb, st, _ in {id(v[1]): v for v in mod.values()}.values():
+                emb.record_stream(main)
+                st.d.record_stream(main)
+                st.side = True
 
         ctx_in = ehs.to(BF16).transpose(0, 1).reshape(L * B, -1)        # rows t*B + b
         hx = torch.cat([self._linear(ctx_in, "context_embedder"), self._linear(tokens, "x_embedder")], 0)

@@ -24,6 +24,7 @@ class ModState:
     def __init__(self, emb: torch.Tensor):
         self.d = torch.empty_like(emb)
         self._owner = False
+        self.side = False   # emb came from the weight-gradient stream (module/flux.py): the adaLN dmod sums go there
 
     def claim(self) -> bool:
         if self._owner:
@@ -108,6 +109,14 @@ def rows_linear(x, segs):
     return RowsLinearFn.apply(x, segs, *_seg_params(segs))
 
 
+def _dmod_side(ctx, x, dy, emb):
+    """the adaLN's modulation-gradient sums on the weight-gradient stream, where the modulation GEMM's backward (its
+    only reader) runs: they leave the dx chain"""
+    with S.wgrad_region((x, dy) + tuple(t for st in ctx.stats for t in st)):
+        for (r0, r1, sh, sc), st in zip(ctx.segs, ctx.stats):
+            K.adaln_dmod(x[r0:r1], dy[r0:r1], emb, sh, sc, ctx.B, st, ctx.state.d)
+
+
 class AdaLNFn(torch.autograd.Function):
     """y[r0:r1] = LN(x[r0:r1]) * (1 + emb[b, scale_off:]) + emb[b, shift_off:] per row segment."""
 
@@ -129,8 +138,11 @@ class AdaLNFn(torch.autograd.Function):
         if dy.stride(1) != 1:
             dy = dy.contiguous()
         dx = torch.empty_like(x)
+        side = ctx.state.side
         for (r0, r1, sh, sc), st in zip(ctx.segs, ctx.stats):
-            K.adaln_bwd(x[r0:r1], dy[r0:r1], emb, sh, sc, ctx.B, st, dmod=ctx.state.d, dx=dx[r0:r1])
+            K.adaln_bwd(x[r0:r1], dy[r0:r1], emb, sh, sc, ctx.B, st, dmod=None if side else ctx.state.d, dx=dx[r0:r1])
+        if side:
+            _dmod_side(ctx, x, dy, emb)
         return dx, (ctx.state.d if ctx.owner else None), None, None, None
 
 
@@ -161,9 +173,12 @@ class AdaLNResFn(torch.autograd.Function):
         if dres is not None and (dres.stride(1) != 1 or dres.stride(0) % 8):
             dres = dres.contiguous()
         dx = torch.empty_like(x)
+        side = ctx.state.side
         for (r0, r1, sh, sc), st in zip(ctx.segs, ctx.stats):
-            K.adaln_bwd(x[r0:r1], dy[r0:r1], emb, sh, sc, ctx.B, st, dmod=ctx.state.d, dx=dx[r0:r1],
+            K.adaln_bwd(x[r0:r1], dy[r0:r1], emb, sh, sc, ctx.B, st, dmod=None if side else ctx.state.d, dx=dx[r0:r1],
                         dres=dres[r0:r1] if dres is not None else None)
+        if side:
+            _dmod_side(ctx, x, dy, emb)
         return dx, (ctx.state.d if ctx.owner else None), None, None, None
 
 
@@ -186,6 +201,8 @@ class GatedAddFn(torch.autograd.Function):
         if dout.stride(1) != 1:
             dout = dout.contiguous()
         dy = torch.empty_like(y)
+        # (with the modulation branch on the weight-gradient stream the gate sums stay here, fused with dy: splitting
+        # them off measured neutral, profiles/r6_flux_mod_side_ab.txt)
         for r0, r1, g in ctx.segs:
             K.gated_add_bwd(dout[r0:r1], y[r0:r1], emb, g, ctx.B, ctx.state.d, dy=dy[r0:r1])
         return dout, dy, (ctx.state.d if ctx.owner else None), None, None, None

@@ -61,6 +61,11 @@ def test_adaln_gated(dev):
     dyv = K.gated_add_bwd(dy, yv, emb, 2 * D, B, dmod)
     assert rel(dyv, yr.grad.reshape(T * B, D)) < 1e-2
     assert rel(dmod[:, 2 * D:], gr.grad) < 2e-2
+    # the split forms (module/flux.py with the modulation branch on the weight-gradient stream): the same bits
+    dmod3 = dmod.clone()
+    dmod3[:, :2 * D] = 0
+    K.adaln_dmod(x, dy, emb, 0, D, B, st, dmod3)
+    assert torch.equal(dmod3, dmod)
 
 
 def test_qknorm_rope(dev):
