@@ -243,10 +243,13 @@ void set_lora_plans(const std::vector<std::vector<int64_t>>& rows) {
 // The entries were measured at M = 4096 / 16384 (one tile per CU or whole waves of them); at the aspect buckets' other
 // row counts a tile grid just past a multiple of the 256 CUs runs a second round for a few tiles (4160 rows on
 // 128x160 tiles: 264 tiles, ~2x the time), so an entry applies only while the grid fills its rounds >= 85 %.
+// An entry for the exact row count (class slot = -M: the aspect buckets' rows, measured) comes first, unchecked.
 int lora_plan(int64_t form, int64_t N, int64_t K, int64_t parts, int64_t M) {
   int tile = 0;
   {
     std::shared_lock<std::shared_mutex> lk(g_lora_plans_mu);
+    auto ex = g_lora_plans.find({form, N, K, parts, -M});
+    if (ex != g_lora_plans.end()) return ex->second;
     auto it = g_lora_plans.find({form, N, K, parts, M >= 8192 ? 1 : 0});
     if (it == g_lora_plans.end()) return 0;
     tile = it->second;

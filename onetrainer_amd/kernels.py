@@ -485,13 +485,20 @@ def _lora_plans() -> dict:
         path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lora_plans_mi355x.json")
         with open(path) as f:
             for e in json.load(f)["plans"]:
-                if e["tile"] > 0 or os.environ.get("OTAMD_LORA_PLANS", "1") != "2":   # =2: fused tiles only
-                    _LORA_PLANS[(e["form"], e["N"], e["K"], e["parts"], e["mclass"])] = e["tile"]
+                mode = os.environ.get("OTAMD_LORA_PLANS", "1")   # A/B: 2 = fused tiles only, 3 = no exact-M rows
+                if (e["tile"] > 0 or mode != "2") and not ("M" in e and mode == "3"):
+                    # an exact row count is keyed as -M in the class slot (ops_host.cpp lora_plan)
+                    cls = -e["M"] if "M" in e else e["mclass"]
+                    _LORA_PLANS[(e["form"], e["N"], e["K"], e["parts"], cls)] = e["tile"]
     return _LORA_PLANS
 
 
 def _lora_plan(form: int, N: int, K: int, parts: int, M: int):
-    """as ops_host.cpp lora_plan: a tile entry applies only while its grid fills its rounds of 256 CUs >= 85 %"""
+    """as ops_host.cpp lora_plan: an exact-row-count entry first; a class entry's tile applies only while its grid fills
+    its rounds of 256 CUs >= 85 %"""
+    exact = _lora_plans().get((form, N, K, parts, -M))
+    if exact is not None:
+        return exact
     tile = _lora_plans().get((form, N, K, parts, int(M >= 8192)))
     if not tile or tile < 0:
         return tile

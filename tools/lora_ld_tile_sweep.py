@@ -43,7 +43,13 @@ def timeit(f, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--ms", default="", help="level-2,level-1 row counts to sweep instead of 4096,16384 (e.g. 4160,16640)")
     a = ap.parse_args()
+    if a.ms:
+        m2, m1 = (int(v) for v in a.ms.split(","))
+        remap = {4096: m2, 16384: m1}
+        FWD[:] = [(remap[M], *rest) for M, *rest in FWD]
+        DGRAD[:] = [(remap[M], *rest) for M, *rest in DGRAD]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     r = 32
