@@ -760,6 +760,7 @@ PYBIND11_MODULE(_otamd_host, m) {
   m.def("linear_lora", &linear_lora);
   m.def("linear_dgrad_lora", &linear_dgrad_lora);
   m.def("set_lora_plans", &set_lora_plans);
+  m.def("lora_plan", &lora_plan);   // the lookup alone (tests: the same answers as kernels._lora_plan)
   m.def("lora_dgrad_fused_counts",
         []() { return std::make_pair((long long)g_lora_dgrad_fused, (long long)g_lora_dgrad_split); });
   m.def("conv2d_lora", &conv2d_lora);

@@ -34,3 +34,18 @@ def test_lookup_rules():
     assert K._lora_plan(0, 10240, 1280, 1, 4096) == -1
     # no entry
     assert K._lora_plan(0, 320, 320, 1, 65536) is None
+
+
+def test_native_lookup_matches_python():
+    h = K._host()
+    if h is None or not hasattr(h, "lora_plan"):
+        import pytest
+        pytest.skip("native host layer not built")
+    for form in (0, 1):
+        for N in (640, 1280, 1920, 2560, 3840, 5120, 10240):
+            for Kd in (640, 1280, 1920, 2560, 3840, 5120, 10240):
+                for parts in (1, 3):
+                    for M in (4, 4032, 4096, 4160, 16128, 16384, 16640, 65536):
+                        want = K._lora_plan(form, N, Kd, parts, M)
+                        got = h.lora_plan(form, N, Kd, parts, M)
+                        assert got == (0 if want is None else want), (form, N, Kd, parts, M)
